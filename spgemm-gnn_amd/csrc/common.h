@@ -1,0 +1,109 @@
+// Shared helpers for the gfx950 MaxK kernels and the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "maxk_hip.h"
+
+namespace maxk {
+
+constexpr int kWave = 64;               // CDNA wavefront width (never 32)
+constexpr int kFwdTileRows = 16;        // destination rows per forward work-group
+constexpr int kFwdThreads = 256;        // 4 waves
+constexpr int kBwdThreads = 512;        // 8 waves
+constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
+
+// Thread-local error message plumbing for maxk_last_error().
+void set_error(const std::string& msg);
+
+#define MAXK_CHECK_ARG(cond, msg)                 \
+  do {                                            \
+    if (!(cond)) {                                \
+      ::maxk::set_error(msg);                     \
+      return MAXK_ERR_INVALID_ARG;                \
+    }                                             \
+  } while (0)
+
+#define MAXK_HIP_TRY(expr)                                                      \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      ::maxk::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));     \
+      return (int)_e;                                                           \
+    }                                                                           \
+  } while (0)
+
+#define MAXK_LAUNCH_CHECK(what)                                                 \
+  do {                                                                          \
+    hipError_t _e = hipGetLastError();                                          \
+    if (_e != hipSuccess) {                                                     \
+      ::maxk::set_error(std::string(what) + ": " + hipGetErrorString(_e));      \
+      return (int)_e;                                                           \
+    }                                                                           \
+  } while (0)
+
+// Forward work item: a run of whole destination rows [row0, row0+nrows) with edge range
+// [e0, e1) = [ptr[row0], ptr[row0+nrows]), or (split=1) one segment of a long row whose
+// partial sum is added atomically into a row pre-zeroed by zero_rows.
+struct FwdTask {
+  int32_t row0;
+  int32_t nrows;
+  int32_t e0;
+  int32_t e1;
+};
+static_assert(sizeof(FwdTask) == 16, "FwdTask is loaded as one dwordx4");
+
+// Backward work item: edges [e0, e1) of the column-block-major edge list, all with
+// source column in [col0, col0 + ncols). shared != 0: more than one work-group owns
+// the block, so the LDS accumulator is flushed with float atomics into a pre-zeroed
+// grad_sp; otherwise it is stored.
+struct BwdTask {
+  int32_t col0;
+  int32_t ncols;
+  int32_t e0;
+  int32_t e1;
+  int32_t shared;
+  int32_t pad[3];
+};
+static_assert(sizeof(BwdTask) == 32, "BwdTask is 2 x dwordx4");
+
+__device__ __forceinline__ void lds_add(float* p, float v) {
+  // Lowers to ds_add_f32 (no return) for an LDS address.
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void global_add(float* p, float v) {
+  // One global_atomic_add_f32 (no CAS loop on gfx950).
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace maxk
+
+// Opaque plan (definition shared by plan.hip and the kernels' launchers).
+struct maxk_plan {
+  int32_t num_nodes = 0;
+  int64_t num_edges = 0;
+  int32_t dim_origin = 0;
+  int32_t dim_k = 0;
+  const int32_t* src_ptr = nullptr;  // identity of the graph the plan was built for
+  const int32_t* src_idx = nullptr;
+  // forward
+  maxk::FwdTask* fwd_tasks = nullptr;
+  int32_t n_fwd_tasks = 0;
+  int32_t* zero_rows = nullptr;  // rows written by split tasks (atomic), zeroed first
+  int32_t n_zero_rows = 0;
+  // backward
+  int32_t bwd_block_cols = 0;
+  int32_t n_bwd_blocks = 0;
+  maxk::BwdTask* bwd_tasks = nullptr;
+  int32_t n_bwd_tasks = 0;
+  int32_t n_bwd_shared = 0;
+  int32_t* bwd_perm = nullptr;   // CSR edge id of each block-major edge
+  int32_t* bwd_row = nullptr;    // destination row r of each block-major edge
+  int32_t* bwd_col = nullptr;    // source column c
+  float* bwd_val = nullptr;      // val snapshot
+  int64_t device_bytes = 0;
+};

@@ -1,0 +1,352 @@
+// Graph plan: the partition metadata the two SpGEMM kernels run on.
+//
+// The reference reads a precomputed ".warp4" file from disk on every call
+// (SPMM_MAXK::do_test SO@0x24bf0 -> cuda_read_array<int> SO@0x252c0; chunk rule SURVEY
+// §8 a4; generator generate_meta.py absent) and never uses the `ptr` it is given. Here the
+// metadata is derived once from the CSR row pointer and the column indices and cached by
+// the caller:
+//
+//   forward : tasks of <= 16 whole rows with <= cap edges (heavy first); rows longer
+//             than cap are split into segments whose outputs are pre-zeroed and summed
+//             with float atomics (the only atomics left in the forward).
+//   backward: a stable radix sort of the edges by source-column block
+//             (hipcub::DeviceRadixSort, keys = idx / block_cols) gives the block-major,
+//             row-sorted edge list {row, col, val}; each block's range is cut into
+//             work-group tasks.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "common.h"
+
+namespace maxk {
+
+size_t bwd_lds_bytes(int block_cols, int k);
+
+constexpr size_t kBwdLdsBudget = 64 * 1024;  // two 512-thread work-groups per CU
+
+__global__ void expand_rows_kernel(const int32_t* __restrict__ ptr, int N,
+                                   int32_t* __restrict__ row_of) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int row = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
+  if (row >= N) return;
+  const int e1 = ptr[row + 1];
+  for (int e = ptr[row] + lane; e < e1; e += kWave) row_of[e] = row;
+}
+
+// Also validates the column ids: any idx outside [0, N) sets *bad (the compute kernels
+// index the CBSR tables with idx and must never read outside them).
+__global__ void block_key_kernel(const int32_t* __restrict__ idx, int64_t E, int C, int N,
+                                 uint32_t* __restrict__ keys, int32_t* __restrict__ ids,
+                                 int* __restrict__ bad) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = idx[e];
+    if (c < 0 || c >= N) atomicOr(bad, 1);
+    const int cc = c < 0 ? 0 : (c >= N ? N - 1 : c);
+    keys[e] = (uint32_t)(cc / C);
+    ids[e] = (int32_t)e;
+  }
+}
+
+__global__ void gather_bwd_kernel(const int32_t* __restrict__ perm,
+                                  const int32_t* __restrict__ row_of,
+                                  const int32_t* __restrict__ idx,
+                                  const float* __restrict__ val, int64_t E,
+                                  int32_t* __restrict__ brow, int32_t* __restrict__ bcol,
+                                  float* __restrict__ bval) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < E;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t e = perm[j];
+    if (brow) brow[j] = row_of[e];
+    if (bcol) bcol[j] = idx[e];
+    bval[j] = val ? val[e] : 1.0f;
+  }
+}
+
+// offs[b] = first position j with skeys[j] >= b, b in [0, nblocks].
+__global__ void block_offsets_kernel(const uint32_t* __restrict__ skeys, int64_t E,
+                                     int nblocks, int64_t* __restrict__ offs) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nblocks) return;
+  int64_t lo = 0, hi = E;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (skeys[mid] < (uint32_t)b) lo = mid + 1; else hi = mid;
+  }
+  offs[b] = lo;
+}
+
+static void dfree(void* q) { if (q) (void)hipFree(q); }
+
+static int grid_for(int64_t n, int threads) {
+  int64_t g = (n + threads - 1) / threads;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 65536));
+}
+
+static void free_plan(maxk_plan* p) {
+  if (!p) return;
+  dfree(p->fwd_tasks);
+  dfree(p->zero_rows);
+  dfree(p->bwd_tasks);
+  dfree(p->bwd_perm);
+  dfree(p->bwd_row);
+  dfree(p->bwd_col);
+  dfree(p->bwd_val);
+  delete p;
+}
+
+// Forward task list from a host copy of ptr.
+static void build_fwd_tasks(const std::vector<int32_t>& hp, int N, std::vector<FwdTask>& tasks,
+                            std::vector<int32_t>& zero_rows) {
+  const int R = kFwdTileRows;
+  const int64_t E = hp[N];
+  const int ntiles = (N + R - 1) / R;
+  const int64_t avg = ntiles ? (E + ntiles - 1) / ntiles : 0;
+  const int64_t cap = std::max<int64_t>(4096, 4 * avg);
+  auto push_rows = [&](int r0, int r1) {
+    if (r1 > r0) tasks.push_back(FwdTask{r0, r1 - r0, hp[r0], hp[r1]});
+  };
+  for (int r0 = 0; r0 < N; r0 += R) {
+    const int r1 = std::min(N, r0 + R);
+    if ((int64_t)hp[r1] - hp[r0] <= cap) {
+      push_rows(r0, r1);
+      continue;
+    }
+    int g0 = r0;
+    for (int r = r0; r < r1; ++r) {
+      const int64_t deg = (int64_t)hp[r + 1] - hp[r];
+      if (deg > cap) {
+        push_rows(g0, r);
+        for (int64_t s = hp[r]; s < hp[r + 1]; s += cap)
+          tasks.push_back(FwdTask{r, -1, (int32_t)s, (int32_t)std::min<int64_t>(s + cap, hp[r + 1])});
+        zero_rows.push_back(r);
+        g0 = r + 1;
+      } else if ((int64_t)hp[r + 1] - hp[g0] > cap) {
+        push_rows(g0, r);
+        g0 = r;
+      }
+    }
+    push_rows(g0, r1);
+  }
+  std::stable_sort(tasks.begin(), tasks.end(), [](const FwdTask& a, const FwdTask& b) {
+    return (a.e1 - a.e0) > (b.e1 - b.e0);
+  });
+}
+
+}  // namespace maxk
+
+using namespace maxk;
+
+extern "C" int maxk_plan_create(const int32_t* ptr, const int32_t* idx, const float* val,
+                                int32_t N, int64_t E, int32_t D, int32_t k, void* stream,
+                                maxk_plan** out_plan) {
+  MAXK_CHECK_ARG(out_plan != nullptr, "maxk_plan_create: out_plan is null");
+  *out_plan = nullptr;
+  MAXK_CHECK_ARG(N >= 0 && E >= 0 && E < (int64_t)INT32_MAX,
+                 "maxk_plan_create: sizes out of range (E must fit int32)");
+  MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_plan_create: dim_origin must be in [1, 256]");
+  MAXK_CHECK_ARG(k >= 1 && k <= D, "k must be between 1 and input dimension");
+  MAXK_CHECK_ARG(ptr != nullptr && (E == 0 || idx != nullptr), "maxk_plan_create: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+
+  maxk_plan* p = new maxk_plan();
+  p->num_nodes = N;
+  p->num_edges = E;
+  p->dim_origin = D;
+  p->dim_k = k;
+  p->src_ptr = ptr;
+  p->src_idx = idx;
+
+  int32_t* row_of = nullptr;
+  uint32_t* keys_in = nullptr;
+  uint32_t* keys_out = nullptr;
+  int32_t* ids_in = nullptr;
+  void* temp = nullptr;
+  int64_t* d_offs = nullptr;
+  int* d_bad = nullptr;
+  auto fail = [&](int rc) {
+    dfree(row_of);
+    dfree(keys_in);
+    dfree(keys_out);
+    dfree(ids_in);
+    dfree(temp);
+    dfree(d_offs);
+    dfree(d_bad);
+    free_plan(p);
+    return rc;
+  };
+#define PLAN_TRY(expr)                                                            \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      set_error(std::string("maxk_plan_create: ") + #expr + ": " + hipGetErrorString(_e)); \
+      return fail((int)_e);                                                       \
+    }                                                                             \
+  } while (0)
+
+  // ---------------- forward
+  std::vector<int32_t> hp(N + 1);
+  PLAN_TRY(hipMemcpyAsync(hp.data(), ptr, sizeof(int32_t) * (N + 1), hipMemcpyDeviceToHost, s));
+  PLAN_TRY(hipStreamSynchronize(s));
+  if (hp[0] != 0 || (int64_t)hp[N] != E) {
+    set_error("maxk_plan_create: ptr[0] must be 0 and ptr[N] must equal num_edges");
+    return fail(MAXK_ERR_INVALID_ARG);
+  }
+  for (int r = 0; r < N; ++r) {
+    if (hp[r + 1] < hp[r]) {
+      set_error("maxk_plan_create: ptr must be non-decreasing");
+      return fail(MAXK_ERR_INVALID_ARG);
+    }
+  }
+  std::vector<FwdTask> ftasks;
+  std::vector<int32_t> zrows;
+  build_fwd_tasks(hp, N, ftasks, zrows);
+  p->n_fwd_tasks = (int32_t)ftasks.size();
+  p->n_zero_rows = (int32_t)zrows.size();
+  if (!ftasks.empty()) {
+    PLAN_TRY(hipMalloc(&p->fwd_tasks, sizeof(FwdTask) * ftasks.size()));
+    PLAN_TRY(hipMemcpyAsync(p->fwd_tasks, ftasks.data(), sizeof(FwdTask) * ftasks.size(),
+                            hipMemcpyHostToDevice, s));
+    p->device_bytes += sizeof(FwdTask) * ftasks.size();
+  }
+  if (!zrows.empty()) {
+    PLAN_TRY(hipMalloc(&p->zero_rows, sizeof(int32_t) * zrows.size()));
+    PLAN_TRY(hipMemcpyAsync(p->zero_rows, zrows.data(), sizeof(int32_t) * zrows.size(),
+                            hipMemcpyHostToDevice, s));
+    p->device_bytes += sizeof(int32_t) * zrows.size();
+  }
+
+  // ---------------- backward
+  const size_t per_col = bwd_lds_bytes(1, k);
+  int C = (int)std::max<size_t>(1, kBwdLdsBudget / per_col);
+  C = std::min(C, std::max(N, 1));
+  const int nblocks = N > 0 ? (N + C - 1) / C : 0;
+  p->bwd_block_cols = C;
+  p->n_bwd_blocks = nblocks;
+  std::vector<int64_t> offs(nblocks + 1, 0);
+  if (E > 0) {
+    PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
+    PLAN_TRY(hipMalloc(&keys_in, sizeof(uint32_t) * E));
+    PLAN_TRY(hipMalloc(&keys_out, sizeof(uint32_t) * E));
+    PLAN_TRY(hipMalloc(&ids_in, sizeof(int32_t) * E));
+    PLAN_TRY(hipMalloc(&p->bwd_perm, sizeof(int32_t) * E));
+    hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
+    PLAN_TRY(hipMalloc(&d_bad, sizeof(int)));
+    PLAN_TRY(hipMemsetAsync(d_bad, 0, sizeof(int), s));
+    hipLaunchKernelGGL(block_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, E, C, N,
+                       keys_in, ids_in, d_bad);
+    PLAN_TRY(hipGetLastError());
+    int end_bit = 1;
+    while ((1 << end_bit) < nblocks) ++end_bit;
+    size_t temp_bytes = 0;
+    PLAN_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, ids_in,
+                                                p->bwd_perm, (int)E, 0, end_bit, s));
+    PLAN_TRY(hipMalloc(&temp, temp_bytes));
+    PLAN_TRY(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, ids_in,
+                                                p->bwd_perm, (int)E, 0, end_bit, s));
+    PLAN_TRY(hipMalloc(&p->bwd_row, sizeof(int32_t) * E));
+    PLAN_TRY(hipMalloc(&p->bwd_col, sizeof(int32_t) * E));
+    PLAN_TRY(hipMalloc(&p->bwd_val, sizeof(float) * E));
+    p->device_bytes += (int64_t)E * 16;
+    hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
+                       p->bwd_perm, row_of, idx, val, E, p->bwd_row, p->bwd_col, p->bwd_val);
+    PLAN_TRY(hipMalloc(&d_offs, sizeof(int64_t) * (nblocks + 1)));
+    hipLaunchKernelGGL(block_offsets_kernel, dim3((nblocks + 256) / 256), dim3(256), 0, s,
+                       keys_out, E, nblocks, d_offs);
+    PLAN_TRY(hipGetLastError());
+    PLAN_TRY(hipMemcpyAsync(offs.data(), d_offs, sizeof(int64_t) * (nblocks + 1),
+                            hipMemcpyDeviceToHost, s));
+    int bad = 0;
+    PLAN_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
+    PLAN_TRY(hipStreamSynchronize(s));
+    if (bad) {
+      set_error("maxk_plan_create: idx contains column ids outside [0, num_nodes)");
+      return fail(MAXK_ERR_INVALID_ARG);
+    }
+  }
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        cus = prop.multiProcessorCount;
+    }
+  }
+  const int64_t desired = (int64_t)cus * 4;
+  const int64_t bcap = std::max<int64_t>(4096, (E + desired - 1) / std::max<int64_t>(desired, 1));
+  std::vector<BwdTask> btasks;
+  int nshared = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    const int64_t o0 = offs[b], o1 = offs[b + 1];
+    const int64_t nnz = o1 - o0;
+    const int nch = (int)std::max<int64_t>(1, (nnz + bcap - 1) / bcap);
+    const int col0 = b * C;
+    const int ncols = std::min(C, N - col0);
+    if (nch > 1) ++nshared;
+    for (int i = 0; i < nch; ++i) {
+      BwdTask t{};
+      t.col0 = col0;
+      t.ncols = ncols;
+      t.e0 = (int32_t)(o0 + nnz * i / nch);
+      t.e1 = (int32_t)(o0 + nnz * (i + 1) / nch);
+      t.shared = nch > 1;
+      btasks.push_back(t);
+    }
+  }
+  std::stable_sort(btasks.begin(), btasks.end(), [](const BwdTask& a, const BwdTask& b) {
+    return (a.e1 - a.e0) > (b.e1 - b.e0);
+  });
+  p->n_bwd_tasks = (int32_t)btasks.size();
+  p->n_bwd_shared = nshared;
+  if (!btasks.empty()) {
+    PLAN_TRY(hipMalloc(&p->bwd_tasks, sizeof(BwdTask) * btasks.size()));
+    PLAN_TRY(hipMemcpyAsync(p->bwd_tasks, btasks.data(), sizeof(BwdTask) * btasks.size(),
+                            hipMemcpyHostToDevice, s));
+    p->device_bytes += sizeof(BwdTask) * btasks.size();
+  }
+  PLAN_TRY(hipStreamSynchronize(s));
+  dfree(row_of);
+  dfree(keys_in);
+  dfree(keys_out);
+  dfree(ids_in);
+  dfree(temp);
+  dfree(d_offs);
+  dfree(d_bad);
+#undef PLAN_TRY
+  *out_plan = p;
+  return MAXK_OK;
+}
+
+extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* stream) {
+  MAXK_CHECK_ARG(p != nullptr, "maxk_plan_refresh_values: plan is null");
+  if (p->num_edges == 0) return MAXK_OK;
+  hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
+                     (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
+                     nullptr, nullptr, p->bwd_val);
+  MAXK_LAUNCH_CHECK("maxk_plan_refresh_values launch");
+  return MAXK_OK;
+}
+
+extern "C" int maxk_plan_get_info(const maxk_plan* p, maxk_plan_info* info) {
+  MAXK_CHECK_ARG(p != nullptr && info != nullptr, "maxk_plan_get_info: null pointer");
+  info->num_nodes = p->num_nodes;
+  info->num_edges = p->num_edges;
+  info->dim_origin = p->dim_origin;
+  info->dim_k = p->dim_k;
+  info->fwd_tasks = p->n_fwd_tasks;
+  info->fwd_split_rows = p->n_zero_rows;
+  info->bwd_block_cols = p->bwd_block_cols;
+  info->bwd_blocks = p->n_bwd_blocks;
+  info->bwd_tasks = p->n_bwd_tasks;
+  info->bwd_shared_blocks = p->n_bwd_shared;
+  info->device_bytes = p->device_bytes;
+  return MAXK_OK;
+}
+
+extern "C" int maxk_plan_destroy(maxk_plan* p) {
+  free_plan(p);
+  return MAXK_OK;
+}

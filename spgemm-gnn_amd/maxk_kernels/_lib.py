@@ -1,0 +1,90 @@
+"""ctypes binding of the C ABI in include/maxk_hip.h (libmaxk_hip.so, built in-tree).
+
+The library is the product: there is no Python or CPU fallback. If the shared object is
+missing or cannot be loaded, importing :mod:`maxk_kernels` raises ImportError, exactly as
+the reference's ``import maxk_kernels`` does when its extension is absent
+(utils/maxk_layers.py:9-14).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  -- must load torch's libamdhip64 before ours (same soname)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MAXK_HIP_LIB", os.path.join(_HERE, "libmaxk_hip.so"))
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+
+# name -> (restype, argtypes); must match include/maxk_hip.h exactly.
+SIGNATURES = {
+    "maxk_abi_version": (ctypes.c_int, []),
+    "maxk_last_error": (ctypes.c_char_p, []),
+    "maxk_topk_cbsr": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
+    "maxk_scatter_backward": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "maxk_plan_create": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp,
+                                        ctypes.POINTER(_vp)]),
+    "maxk_plan_refresh_values": (ctypes.c_int, [_vp, _vp, _vp]),
+    "maxk_plan_get_info": (ctypes.c_int, [_vp, _vp]),
+    "maxk_plan_destroy": (ctypes.c_int, [_vp]),
+    "maxk_spgemm_forward": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
+                                           _i32, _i32, _vp]),
+    "maxk_sspmm_backward": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
+                                           _i32, _i32, _vp]),
+    "maxk_dense_spmm_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),
+    "maxk_warp4_build": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
+}
+
+
+class PlanInfo(ctypes.Structure):
+    """Mirror of ``maxk_plan_info``."""
+
+    _fields_ = [
+        ("num_nodes", _i32),
+        ("num_edges", _i64),
+        ("dim_origin", _i32),
+        ("dim_k", _i32),
+        ("fwd_tasks", _i32),
+        ("fwd_split_rows", _i32),
+        ("bwd_block_cols", _i32),
+        ("bwd_blocks", _i32),
+        ("bwd_tasks", _i32),
+        ("bwd_shared_blocks", _i32),
+        ("device_bytes", _i64),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"maxk_kernels: native library {LIB_PATH} is missing; build it with "
+            "`make -C spgemm-gnn_amd` (or __graft_entry__.build())")
+    try:
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    except OSError as exc:  # pragma: no cover - depends on the box
+        raise ImportError(f"maxk_kernels: cannot load {LIB_PATH}: {exc}") from exc
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class MaxKError(RuntimeError):
+    """Raised for a non-zero return of the C ABI."""
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib.maxk_last_error()
+        msg = msg.decode() if msg else ""
+        raise MaxKError(f"maxk_kernels: {what} failed (code {rc}): {msg}")

@@ -1,0 +1,117 @@
+"""Synthetic graphs with the benchmark datasets' (N, E) — no datasets are available offline.
+
+Generator: per-row in-degrees from a seeded lognormal
+(sigma 1.2; the reference publishes no degree histogram) scaled so that sum(deg) = E - N,
+columns drawn uniformly without replacement (excluding the row itself) and sorted, plus
+one self-loop per row (DGL ``AddSelfLoop``: run/reddit.log:28 reports 114,848,857 edges
+after it). Seed 97 is the reference default (utils/config.py:54).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+DATASETS = {
+    # name: (num_nodes, num_edges incl. self-loops)   sources: SURVEY §6 / spgemm_plot.py
+    "reddit": (232_965, 114_848_857),
+    "ogbn-products": (2_449_029, 123_718_280),
+    "ogbn-proteins": (132_534, 79_122_504),
+    "flickr": (89_250, 989_006 + 89_250),
+    "yelp": (716_847, 13_954_819 + 716_847),
+}
+
+
+def lognormal_degrees(n: int, total: int, sigma: float, gen: torch.Generator,
+                      device) -> torch.Tensor:
+    """int64 [n] degrees in [0, n-1] summing exactly to ``total``."""
+    if n <= 1:
+        return torch.zeros(n, dtype=torch.int64, device=device)
+    total = min(total, n * (n - 1))
+    z = torch.randn(n, generator=gen, device=device, dtype=torch.float64)
+    w = torch.exp(sigma * z)
+    exact = w / w.sum() * total
+    deg = torch.floor(exact).clamp_(max=n - 1).to(torch.int64)
+    rem = int(total - int(deg.sum()))
+    while rem > 0:
+        room = deg < (n - 1)
+        frac = torch.where(room, exact - deg.to(torch.float64), torch.full_like(exact, -1.0))
+        take = min(rem, int(room.sum()))
+        top = torch.topk(frac, take).indices
+        deg[top] += 1
+        rem -= take
+    return deg
+
+
+def synthetic_csr(num_nodes: int, num_edges: int, seed: int = 97, sigma: float = 1.2,
+                  device="cpu", self_loops: bool = True):
+    """Destination-row CSR (ptr int32 [N+1], idx int32 [E]) with sorted columns."""
+    device = torch.device(device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    n = int(num_nodes)
+    extra = n if self_loops else 0
+    deg = lognormal_degrees(n, int(num_edges) - extra, sigma, gen, device)
+    m = int(deg.sum())
+    rows = torch.repeat_interleave(torch.arange(n, device=device), deg)
+    # s ~ U{0 .. n-2-deg}: a sorted multiset of deg draws; t_i = s_i + i is then a sorted
+    # deg-subset of [0, n-1); shifting t >= row by one excludes the row itself.
+    span = (n - 1 - deg)[rows] + 1
+    s = torch.floor(torch.rand(m, generator=gen, device=device, dtype=torch.float64)
+                    * span.to(torch.float64)).to(torch.int64)
+    s = torch.minimum(s, span - 1)
+    key = rows * n + s
+    key, _ = torch.sort(key)
+    s = key - rows * n
+    start = torch.cumsum(deg, 0) - deg
+    local = torch.arange(m, device=device) - start[rows]
+    cols = s + local
+    cols = cols + (cols >= rows).to(torch.int64)
+    del key, s, local, span
+    if self_loops:
+        ar = torch.arange(n, device=device)
+        rows = torch.cat([rows, ar])
+        cols = torch.cat([cols, ar])
+        key, _ = torch.sort(rows * n + cols)
+        rows = key // n
+        cols = key - rows * n
+        deg = deg + 1
+        del key
+    ptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    ptr[1:] = torch.cumsum(deg, 0)
+    return ptr.to(torch.int32), cols.to(torch.int32)
+
+
+def row_degrees(ptr: torch.Tensor) -> torch.Tensor:
+    return (ptr[1:] - ptr[:-1]).to(torch.int64)
+
+
+def sage_mean_values(ptr: torch.Tensor) -> torch.Tensor:
+    """val[nz] = 1/deg(row) (SAGE mean; utils/maxk_layers.py:147-157)."""
+    deg = row_degrees(ptr)
+    inv = 1.0 / deg.clamp(min=1).to(torch.float32)
+    return torch.repeat_interleave(inv, deg)
+
+
+def gcn_values(ptr: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """val[nz] = deg(r)^-1/2 * deg(c)^-1/2 (symmetric GCN normalisation with in-degrees;
+    utils/maxk_layers.py:314-317,373-376)."""
+    deg = row_degrees(ptr).clamp(min=1).to(torch.float32)
+    nr = deg.rsqrt()
+    rows = torch.repeat_interleave(torch.arange(deg.numel(), device=ptr.device),
+                                   row_degrees(ptr))
+    return nr[rows] * nr[idx.to(torch.int64)]
+
+
+def features(num_nodes: int, dim: int, seed: int, device="cpu",
+             gen_device: Optional[str] = None) -> torch.Tensor:
+    """N(0, 1) f32 [num_nodes, dim] from a seeded generator."""
+    gd = torch.device(gen_device or device)
+    g = torch.Generator(device=gd)
+    g.manual_seed(seed)
+    return torch.randn(num_nodes, dim, generator=g, device=gd).to(device)
+
+
+def dataset_csr(name: str, device="cpu", seed: int = 97):
+    n, e = DATASETS[name]
+    return synthetic_csr(n, e, seed=seed, device=device)

@@ -1,0 +1,249 @@
+"""The four functions of the reference's ``maxk_kernels`` extension, on the gfx950 C ABI.
+
+Reference binding: pybind11 module ``maxk_kernels`` (PyInit SO@0xfc90) with the wrappers
+``maxk_forward`` (SO@0xe340), ``maxk_backward`` (SO@0xe690), ``spgemm_forward``
+(SO@0xea20) and ``spgemm_backward`` (SO@0xf170); argument checks recovered from
+``kernels/maxk_bindings.cpp`` lines 27-30, 34-36, 45-54, 65-71.
+
+Same names, same positional signatures, same return shapes and the same RuntimeError
+messages for the same checks. Differences (all fixes of SURVEY §8(b) defects):
+
+* kernels are launched on the current HIP stream with no device-wide synchronisation;
+* ``spgemm_forward/backward`` derive their partition metadata from ``ptr`` (cached per
+  graph) instead of reading ``../w12_nz64_warp_4/graph.warp4`` and printing to stdout;
+* ``maxk_backward`` returns a stable ``[N, D]`` shape when ``dim_origin`` is given;
+* ``maxk_forward`` can also return ``sp_index`` (the reference computes and drops it).
+"""
+from __future__ import annotations
+
+import collections
+import ctypes
+import threading
+from typing import Optional, Tuple
+
+import torch
+
+from ._lib import PlanInfo, check, lib
+
+TOPK_MODES = {"exact": 0, "ref_compat": 1}
+
+
+def _stream() -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t: Optional[torch.Tensor]) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+def _need(cond: bool, msg: str) -> None:
+    if not cond:
+        raise RuntimeError(msg)
+
+
+def _check_tensor(t: torch.Tensor, name: str, dtype: Optional[torch.dtype] = None) -> None:
+    _need(isinstance(t, torch.Tensor), f"{name} must be a tensor")
+    _need(t.is_cuda, f"{name} must be a CUDA tensor")
+    _need(t.is_contiguous(), f"{name} must be contiguous")
+    if dtype is not None:
+        _need(t.dtype == dtype, f"{name} must be {str(dtype).replace('torch.', '')}")
+
+
+# -------------------------------------------------------------------------------------
+# MaxK top-k
+# -------------------------------------------------------------------------------------
+def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
+                 return_index: bool = False):
+    """MaxK nonlinearity -> CBSR. Reference: ``maxk_forward(input, k) -> [N, k] f32``.
+
+    Checks (bindings.cpp:27-30): "input must be a CUDA tensor", "input must be
+    contiguous", "Input must be 2D tensor", "k must be between 1 and input dimension".
+    ``mode='exact'`` selects the true top-k (utils/models.py:14 semantics), ``'ref_compat'``
+    the reference kernel's 8-step bisection, bit-exact. With ``return_index=True`` returns
+    ``(sp_data, sp_index)`` with ``sp_index`` u8 ``[N, k]`` in ascending feature order.
+    """
+    _need(input.is_cuda, "input must be a CUDA tensor")
+    _need(input.is_contiguous(), "input must be contiguous")
+    _need(input.dim() == 2, "Input must be 2D tensor")
+    n, d = input.shape
+    _need(1 <= k <= d, "k must be between 1 and input dimension")
+    _need(d <= 256, "input dimension must be <= 256 (u8 selectors)")
+    _need(input.dtype == torch.float32, "input must be float32")
+    _need(mode in TOPK_MODES, f"mode must be one of {sorted(TOPK_MODES)}")
+    sp_data = torch.empty((n, k), dtype=torch.float32, device=input.device)
+    sp_index = torch.empty((n, k), dtype=torch.uint8, device=input.device)
+    with torch.cuda.device(input.device):
+        check(lib.maxk_topk_cbsr(_p(input), _p(sp_data), _p(sp_index), n, d, k,
+                                 TOPK_MODES[mode], _stream()), "maxk_forward")
+    return (sp_data, sp_index) if return_index else sp_data
+
+
+def maxk_backward(grad_output: torch.Tensor, indices: torch.Tensor,
+                  dim_origin: Optional[int] = None) -> torch.Tensor:
+    """Dense gradient of MaxK from the ``[N, k]`` CBSR gradient.
+
+    Reference (maxk_backward_cuda SO@0x21410): ``g = zeros(N, max(indices)+1)``;
+    ``g[i, indices[i, j]] = grad_output[i, j]`` for j ascending. Checks (bindings.cpp:34-36):
+    grad_output CUDA/contiguous/2-D, indices CUDA/contiguous. Here one device kernel does
+    the scatter; pass ``dim_origin`` for a stable ``[N, dim_origin]`` shape (without it the
+    reference's data-dependent width ``max(indices)+1`` is kept, which costs a host sync).
+    """
+    _need(grad_output.is_cuda, "grad_output must be a CUDA tensor")
+    _need(grad_output.is_contiguous(), "grad_output must be contiguous")
+    _need(grad_output.dim() == 2, "grad_output must be 2D tensor")
+    _need(indices.is_cuda, "indices must be a CUDA tensor")
+    _need(indices.is_contiguous(), "indices must be contiguous")
+    _need(indices.shape == grad_output.shape, "indices must have the shape of grad_output")
+    _need(grad_output.dtype == torch.float32, "grad_output must be float32")
+    n, k = grad_output.shape
+    if indices.dtype != torch.uint8:
+        _need(not indices.dtype.is_floating_point, "indices must be an integer tensor")
+        indices = indices.to(torch.uint8)
+    if dim_origin is None:
+        dim_origin = int(indices.max().item()) + 1 if indices.numel() else 1
+    _need(1 <= k <= dim_origin <= 256, "k must be between 1 and input dimension")
+    grad_in = torch.empty((n, dim_origin), dtype=torch.float32, device=grad_output.device)
+    with torch.cuda.device(grad_output.device):
+        check(lib.maxk_scatter_backward(_p(grad_output), _p(indices), _p(grad_in), n,
+                                        dim_origin, k, _stream()), "maxk_backward")
+    return grad_in
+
+
+# -------------------------------------------------------------------------------------
+# graph plans (cached partition metadata)
+# -------------------------------------------------------------------------------------
+class GraphPlan:
+    """Owns one ``maxk_plan`` (device partition metadata for a CSR graph, k and D)."""
+
+    def __init__(self, ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k):
+        self.handle = ctypes.c_void_p(0)
+        self.device = ptr.device
+        self._refs = (ptr, idx, val)  # keep the graph's storage alive while cached
+        self.val_version = val._version if val is not None else -1
+        with torch.cuda.device(ptr.device):
+            check(lib.maxk_plan_create(_p(ptr), _p(idx), _p(val), num_nodes, num_edges,
+                                       dim_origin, dim_k, _stream(),
+                                       ctypes.byref(self.handle)), "maxk_plan_create")
+
+    def refresh_values(self, val: torch.Tensor) -> None:
+        with torch.cuda.device(self.device):
+            check(lib.maxk_plan_refresh_values(self.handle, _p(val), _stream()),
+                  "maxk_plan_refresh_values")
+        self._refs = (self._refs[0], self._refs[1], val)
+        self.val_version = val._version
+
+    def info(self) -> dict:
+        info = PlanInfo()
+        check(lib.maxk_plan_get_info(self.handle, ctypes.byref(info)), "maxk_plan_get_info")
+        return info.as_dict()
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            lib.maxk_plan_destroy(h)
+            self.handle = ctypes.c_void_p(0)
+
+
+_PLAN_CACHE: "collections.OrderedDict[tuple, GraphPlan]" = collections.OrderedDict()
+_PLAN_CACHE_SIZE = 8
+_PLAN_LOCK = threading.Lock()
+
+
+def get_plan(ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k) -> GraphPlan:
+    """Cached plan for (graph storage, structure version, k, D); val changes are picked up
+    through ``val._version`` (in-place edits) or a new ``val`` tensor."""
+    key = (ptr.device.index, ptr.data_ptr(), idx.data_ptr(), ptr._version, idx._version,
+           int(num_nodes), int(num_edges), int(dim_origin), int(dim_k))
+    with _PLAN_LOCK:
+        plan = _PLAN_CACHE.get(key)
+        if plan is not None:
+            _PLAN_CACHE.move_to_end(key)
+            cached_val = plan._refs[2]
+            if cached_val is not val or plan.val_version != val._version:
+                plan.refresh_values(val)
+            return plan
+        plan = GraphPlan(ptr, idx, val, int(num_nodes), int(num_edges), int(dim_origin),
+                         int(dim_k))
+        _PLAN_CACHE[key] = plan
+        while len(_PLAN_CACHE) > _PLAN_CACHE_SIZE:
+            _PLAN_CACHE.popitem(last=False)
+        return plan
+
+
+def clear_plan_cache() -> None:
+    with _PLAN_LOCK:
+        _PLAN_CACHE.clear()
+
+
+def _check_graph(ptr, idx, val, num_nodes, num_edges):
+    _check_tensor(ptr, "ptr", torch.int32)
+    _check_tensor(idx, "idx", torch.int32)
+    _check_tensor(val, "val", torch.float32)
+    _need(ptr.dim() == 1 and ptr.numel() == num_nodes + 1, "ptr must have num_nodes+1 entries")
+    _need(idx.numel() == num_edges and val.numel() == num_edges,
+          "idx and val must have num_edges entries")
+
+
+# -------------------------------------------------------------------------------------
+# SpGEMM forward / SSpMM backward
+# -------------------------------------------------------------------------------------
+def spgemm_forward(ptr, idx, val, sp_data, sp_index, num_nodes: int, num_edges: int,
+                   dim_k: int, dim_origin: int, plan: Optional[GraphPlan] = None
+                   ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Row-wise-product SpGEMM over CBSR features.
+
+    Reference ``spgemm_forward(ptr, idx, val, sp_data, sp_index, num_nodes, num_edges,
+    dim_k, dim_origin) -> (out[num_nodes, dim_origin], sp_index)`` (spgemm_forward_cuda
+    SO@0x221a0; checks bindings.cpp:45-54): ``out[r] = sum_nz val[nz] *
+    densify(sp_data[idx[nz]], sp_index[idx[nz]])``.
+    """
+    _check_graph(ptr, idx, val, num_nodes, num_edges)
+    _check_tensor(sp_data, "sp_data", torch.float32)
+    _check_tensor(sp_index, "sp_index", torch.uint8)
+    _need(sp_data.shape == (num_nodes, dim_k) and sp_index.shape == (num_nodes, dim_k),
+          "sp_data and sp_index must be [num_nodes, dim_k]")
+    _need(1 <= dim_k <= dim_origin <= 256, "k must be between 1 and input dimension")
+    if plan is None:
+        plan = get_plan(ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k)
+    out = torch.empty((num_nodes, dim_origin), dtype=torch.float32, device=sp_data.device)
+    with torch.cuda.device(sp_data.device):
+        check(lib.maxk_spgemm_forward(plan.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
+                                      _p(sp_index), _p(out), num_nodes, num_edges, dim_k,
+                                      dim_origin, _stream()), "spgemm_forward")
+    return out, sp_index
+
+
+def spgemm_backward(ptr, idx, val, grad_output, sp_index, num_nodes: int, num_edges: int,
+                    dim_k: int, dim_origin: int, plan: Optional[GraphPlan] = None
+                    ) -> torch.Tensor:
+    """Outer-product SSpMM: ``grad_sp[c, l] = sum_{(r,c)} val * grad_output[r, sp_index[c, l]]``.
+
+    Reference ``spgemm_backward(ptr, idx, val, grad_output, sp_index, num_nodes,
+    num_edges, dim_k, dim_origin) -> [num_nodes, dim_k]`` (spgemm_backward_cuda
+    SO@0x22490; checks bindings.cpp:65-71).
+    """
+    _check_graph(ptr, idx, val, num_nodes, num_edges)
+    _check_tensor(grad_output, "grad_output", torch.float32)
+    _check_tensor(sp_index, "sp_index", torch.uint8)
+    _need(grad_output.shape == (num_nodes, dim_origin), "grad_output must be [num_nodes, dim_origin]")
+    _need(sp_index.shape == (num_nodes, dim_k), "sp_index must be [num_nodes, dim_k]")
+    _need(1 <= dim_k <= dim_origin <= 256, "k must be between 1 and input dimension")
+    if plan is None:
+        plan = get_plan(ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k)
+    grad_sp = torch.empty((num_nodes, dim_k), dtype=torch.float32, device=grad_output.device)
+    with torch.cuda.device(grad_output.device):
+        check(lib.maxk_sspmm_backward(plan.handle, _p(ptr), _p(idx), _p(val), _p(grad_output),
+                                      _p(sp_index), _p(grad_sp), num_nodes, num_edges, dim_k,
+                                      dim_origin, _stream()), "spgemm_backward")
+    return grad_sp
+
+
+def dense_spmm(ptr, idx, val, x) -> torch.Tensor:
+    """Dense CSR SpMM comparator (DGL ``update_all(copy_u, sum)`` with edge weights)."""
+    _check_tensor(x, "x", torch.float32)
+    _check_graph(ptr, idx, val, x.shape[0], idx.numel())
+    y = torch.empty_like(x)
+    with torch.cuda.device(x.device):
+        check(lib.maxk_dense_spmm_csr(_p(ptr), _p(idx), _p(val), _p(x), _p(y), x.shape[0],
+                                      x.shape[1], _stream()), "dense_spmm")
+    return y

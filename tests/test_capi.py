@@ -1,0 +1,110 @@
+"""CPU: the C-ABI library loads, exports every declared symbol, and rejects bad arguments
+on the host (no compute call reaches a GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import maxk_kernels
+from maxk_kernels import _lib
+from oracle import oracle
+from maxk_kernels import graphs, warp4
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "maxk_hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(maxk_\w+)\s*\(", text)))
+
+
+def test_library_is_in_tree_and_loaded():
+    assert os.path.exists(_lib.LIB_PATH)
+    assert _lib.LIB_PATH.startswith(os.path.join(ROOT, "spgemm-gnn_amd"))
+    assert maxk_kernels.ABI_VERSION == 1
+
+
+def test_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 12
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), n
+    # and the ctypes binding covers exactly the header
+    assert set(names) == set(_lib.SIGNATURES)
+
+
+def test_library_targets_gfx950():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+@pytest.mark.parametrize("args", [
+    (0, 256, 16, 0),      # ok size-0 -> MAXK_OK without touching the GPU
+])
+def test_topk_zero_rows_is_noop(args):
+    n, d, k, mode = args
+    assert _lib.lib.maxk_topk_cbsr(None, None, None, n, d, k, mode, None) == 0
+
+
+@pytest.mark.parametrize("n,d,k,mode,expect", [
+    (10, 256, 0, 0, -1),    # k < 1
+    (10, 256, 257, 0, -1),  # k > D
+    (10, 300, 8, 0, -1),    # D > 256 (u8 selectors)
+    (10, 256, 8, 7, -1),    # unknown mode
+    (10, 256, 8, 0, -1),    # null pointers
+])
+def test_topk_argument_errors(n, d, k, mode, expect):
+    rc = _lib.lib.maxk_topk_cbsr(None, None, None, n, d, k, mode, None)
+    assert rc == expect
+    msg = _lib.lib.maxk_last_error().decode()
+    assert msg
+
+
+def test_reference_error_message_for_k():
+    _lib.lib.maxk_topk_cbsr(None, None, None, 4, 64, 65, 0, None)
+    assert "k must be between 1 and input dimension" in _lib.lib.maxk_last_error().decode()
+
+
+def test_plan_create_argument_errors():
+    h = ctypes.c_void_p(0)
+    assert _lib.lib.maxk_plan_create(None, None, None, 10, 100, 256, 16, None,
+                                     ctypes.byref(h)) == -1
+    assert _lib.lib.maxk_plan_create(None, None, None, 10, 100, 256, 300, None,
+                                     ctypes.byref(h)) == -1
+    assert _lib.lib.maxk_plan_create(None, None, None, 10, 100, 256, 16, None, None) == -1
+    assert not h.value
+
+
+def test_spgemm_rejects_null_plan():
+    rc = _lib.lib.maxk_spgemm_forward(None, None, None, None, None, None, None, 10, 100, 16,
+                                      256, None)
+    assert rc == -1
+
+
+def test_warp4_build_matches_oracle():
+    ptr, _ = graphs.synthetic_csr(700, 30_000, seed=3)
+    t = warp4.build_warp4(ptr)
+    assert np.array_equal(t, oracle.warp4(ptr.numpy()))
+    # the reference's consumer derives num_warps = bytes / 16 and grid = ceil(W / 12)
+    assert t.shape[1] == 4 and (t[:, 3] == 0).all() and (t[:, 2] <= 64).all()
+
+
+def test_warp4_file_roundtrip(tmp_path):
+    ptr, _ = graphs.synthetic_csr(100, 2000, seed=4)
+    t = warp4.build_warp4(ptr)
+    p = warp4.warp4_path("graph", str(tmp_path))
+    warp4.write_warp4(p, t)
+    assert os.path.getsize(p) == t.size * 4
+    assert np.array_equal(warp4.read_warp4(p), t)
+
+
+def test_python_checks_mirror_reference_messages():
+    import torch
+    x = torch.zeros(4, 8)
+    with pytest.raises(RuntimeError, match="input must be a CUDA tensor"):
+        maxk_kernels.maxk_forward(x, 2)

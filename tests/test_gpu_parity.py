@@ -1,0 +1,261 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the CPU oracle.
+
+Bars (BASELINE.json north_star): top-k index output bit-exact (and its values, which are
+copies); fp32 accumulators within 1e-5 relative, judged per element against the sum of
+absolute terms that fed it (oracle.close_enough).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import maxk_kernels as mk
+from maxk_kernels import graphs
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "maxk_small.npz")
+RTOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with np.load(GOLDEN, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def to_dev(a, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(dev)
+
+
+def assert_close(got, ref, mag, rtol=RTOL):
+    got = got.detach().cpu().numpy() if torch.is_tensor(got) else got
+    ok, worst = oracle.close_enough(got, ref, mag, rtol=rtol)
+    assert ok, f"worst err/bound = {worst:.3g}"
+
+
+def graph_on(dev, ptr, idx, val):
+    return to_dev(ptr, dev), to_dev(idx, dev), to_dev(val, dev)
+
+
+def heavy_graph(n=6000, e=60_000, heavy_rows=(17, 4000), seed=21):
+    """Synthetic graph plus rows connected to every node: rows longer than the forward
+    task cap (4096) are split into segments (the atomic path)."""
+    ptr, idx = graphs.synthetic_csr(n, e, seed=seed)
+    rows = []
+    p = ptr.numpy()
+    ix = idx.numpy()
+    for r in range(n):
+        rows.append(np.arange(n, dtype=np.int32) if r in heavy_rows else ix[p[r]:p[r + 1]])
+    deg = np.array([len(x) for x in rows])
+    ptr2 = np.zeros(n + 1, np.int32)
+    ptr2[1:] = np.cumsum(deg)
+    idx2 = np.concatenate(rows).astype(np.int32)
+    val = np.random.RandomState(seed).uniform(0.1, 1.0, idx2.size).astype(np.float32)
+    return ptr2, idx2, val
+
+
+def empty_rows_graph(n=3000, seed=22):
+    rs = np.random.RandomState(seed)
+    deg = rs.poisson(3, n)
+    deg[rs.rand(n) < 0.3] = 0
+    deg[:40] = 0        # a whole empty forward tile
+    ptr = np.zeros(n + 1, np.int32)
+    ptr[1:] = np.cumsum(deg)
+    idx = np.concatenate([np.sort(rs.choice(n, d, replace=False)) for d in deg]).astype(np.int32)
+    val = rs.randn(idx.size).astype(np.float32)
+    return ptr, idx, val
+
+
+# ------------------------------------------------------------------------ top-k
+@pytest.mark.parametrize("k", [8, 16, 24, 32, 64])
+@pytest.mark.parametrize("mode", ["exact", "ref_compat"])
+def test_topk_golden_bit_exact(gpu, golden, k, mode):
+    h = to_dev(golden["h"], gpu)
+    d, i = mk.maxk_forward(h, k, mode=mode, return_index=True)
+    pre = "exact" if mode == "exact" else "ref"
+    assert np.array_equal(i.cpu().numpy(), golden[f"{pre}_index_k{k}"])
+    assert np.array_equal(d.cpu().numpy(), golden[f"{pre}_data_k{k}"])
+
+
+@pytest.mark.parametrize("d", [256, 128, 64, 100, 7])
+@pytest.mark.parametrize("mode", ["exact", "ref_compat"])
+def test_topk_random_bit_exact(gpu, d, mode):
+    x = graphs.features(4099, d, seed=d)
+    x[5, :] = 0.5                                   # a fully tied row
+    x[6, : d // 2] = -0.0
+    for k in sorted({1, min(d, 3), min(d, 16), min(d, 32), d}):
+        gd, gi = mk.maxk_forward(x.to(gpu), k, mode=mode, return_index=True)
+        od, oi = oracle.maxk(x.numpy(), k, mode)
+        assert np.array_equal(gi.cpu().numpy(), oi), (d, k)
+        assert np.array_equal(gd.cpu().numpy(), od), (d, k)
+
+
+def test_topk_default_returns_reference_shape(gpu):
+    x = graphs.features(10, 64, seed=1).to(gpu)
+    out = mk.maxk_forward(x, 16)
+    assert out.shape == (10, 16) and out.dtype == torch.float32
+
+
+@pytest.mark.parametrize("k", [8, 16, 24, 32, 64])
+def test_maxk_backward_golden(gpu, golden, k):
+    gs = to_dev(golden[f"bwd_k{k}"], gpu)
+    i = to_dev(golden[f"exact_index_k{k}"], gpu)
+    out = mk.maxk_backward(gs, i, dim_origin=256)
+    assert np.array_equal(out.cpu().numpy(), golden[f"maxk_bwd_k{k}"])
+
+
+def test_maxk_backward_repeated_index_and_reference_width(gpu):
+    g = torch.tensor([[1.0, 2.0, 3.0], [4.0, 5.0, 6.0]], device=gpu)
+    i = torch.tensor([[4, 1, 4], [0, 2, 9]], device=gpu, dtype=torch.int64)
+    out = mk.maxk_backward(g, i)          # reference width: max(indices) + 1 = 10
+    assert out.shape == (2, 10)
+    ref = oracle.maxk_backward(g.cpu().numpy(), i.cpu().numpy().astype(np.uint8), 10)
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+# ------------------------------------------------------------------------ SpGEMM forward
+@pytest.mark.parametrize("k", [16, 24])
+def test_spgemm_forward_golden(gpu, golden, k):
+    ptr, idx, val = graph_on(gpu, golden["ptr"], golden["idx"], golden["val"])
+    d = to_dev(golden[f"exact_data_k{k}"], gpu)
+    i = to_dev(golden[f"exact_index_k{k}"], gpu)
+    n = ptr.numel() - 1
+    out, si = mk.spgemm_forward(ptr, idx, val, d, i, n, idx.numel(), k, 256)
+    assert si is i
+    assert_close(out, golden[f"fwd_k{k}"], golden[f"fwd_mag_k{k}"])
+
+
+GRAPHS = {
+    "synthetic": lambda: (lambda p, i: (p.numpy(), i.numpy(),
+                                        graphs.sage_mean_values(p).numpy()))(
+        *graphs.synthetic_csr(5000, 120_000, seed=31)),
+    "heavy_split": heavy_graph,
+    "empty_rows": empty_rows_graph,
+    "single_node": lambda: (np.array([0, 1], np.int32), np.array([0], np.int32),
+                            np.array([0.5], np.float32)),
+}
+
+
+@pytest.mark.parametrize("gname", list(GRAPHS))
+@pytest.mark.parametrize("d,k", [(256, 8), (256, 16), (256, 32), (256, 64), (256, 24),
+                                 (64, 16), (100, 10), (128, 70), (256, 256)])
+def test_spgemm_forward_vs_oracle(gpu, gname, d, k):
+    p, ix, v = GRAPHS[gname]()
+    n = p.size - 1
+    x = graphs.features(n, d, seed=k)
+    od, oi = oracle.maxk(x.numpy(), k)
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    out, _ = mk.spgemm_forward(ptr, idx, val, to_dev(od, gpu), to_dev(oi, gpu), n, ix.size,
+                               k, d)
+    assert_close(out, ref, mag)
+
+
+def test_spgemm_forward_duplicate_selectors_summed(gpu):
+    p = np.array([0, 2, 3], np.int32)
+    ix = np.array([0, 1, 1], np.int32)
+    v = np.array([1.0, 2.0, 0.5], np.float32)
+    data = np.array([[1.0, 10.0, 2.0, 3.0], [3.0, 4.0, 1.0, 1.0]], np.float32)
+    index = np.array([[5, 5, 5, 1], [0, 7, 7, 7]], np.uint8)
+    ref, mag = oracle.spgemm_forward(p, ix, v, data, index, 8, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    out, _ = mk.spgemm_forward(ptr, idx, val, to_dev(data, gpu), to_dev(index, gpu), 2, 3, 4, 8)
+    assert_close(out, ref, mag)
+
+
+# ------------------------------------------------------------------------ SSpMM backward
+@pytest.mark.parametrize("k", [8, 16, 24, 32, 64])
+def test_sspmm_backward_golden(gpu, golden, k):
+    ptr, idx, val = graph_on(gpu, golden["ptr"], golden["idx"], golden["val"])
+    g = to_dev(golden["g"], gpu)
+    i = to_dev(golden[f"exact_index_k{k}"], gpu)
+    n = ptr.numel() - 1
+    gs = mk.spgemm_backward(ptr, idx, val, g, i, n, idx.numel(), k, 256)
+    assert gs.shape == (n, k)
+    assert_close(gs, golden[f"bwd_k{k}"], golden[f"bwd_mag_k{k}"])
+
+
+@pytest.mark.parametrize("gname", list(GRAPHS))
+@pytest.mark.parametrize("d,k", [(256, 8), (256, 16), (256, 32), (256, 64), (256, 24),
+                                 (64, 16), (100, 10), (128, 70), (256, 256)])
+def test_sspmm_backward_vs_oracle(gpu, gname, d, k):
+    p, ix, v = GRAPHS[gname]()
+    n = p.size - 1
+    x = graphs.features(n, d, seed=k)
+    g = graphs.features(n, d, seed=k + 1)
+    _, oi = oracle.maxk(x.numpy(), k)
+    ref, mag = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    gs = mk.spgemm_backward(ptr, idx, val, g.to(gpu), to_dev(oi, gpu), n, ix.size, k, d)
+    assert_close(gs, ref, mag)
+
+
+def test_plan_picks_up_value_changes(gpu):
+    p, ix, v = GRAPHS["synthetic"]()
+    n = p.size - 1
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    x = graphs.features(n, 256, seed=3)
+    g = graphs.features(n, 256, seed=4)
+    od, oi = oracle.maxk(x.numpy(), 16)
+    d_sp, i_sp, gg = to_dev(od, gpu), to_dev(oi, gpu), g.to(gpu)
+    mk.spgemm_backward(ptr, idx, val, gg, i_sp, n, ix.size, 16, 256)
+    val.mul_(3.0)                         # in place: same pointer, new _version
+    v3 = val.cpu().numpy()
+    gs = mk.spgemm_backward(ptr, idx, val, gg, i_sp, n, ix.size, 16, 256)
+    ref, mag = oracle.sspmm_backward(p, ix, v3, g.numpy(), oi, with_mag=True)
+    assert_close(gs, ref, mag)
+    out, _ = mk.spgemm_forward(ptr, idx, val, d_sp, i_sp, n, ix.size, 16, 256)
+    ref, mag = oracle.spgemm_forward(p, ix, v3, od, oi, 256, with_mag=True)
+    assert_close(out, ref, mag)
+
+
+def test_plan_info(gpu):
+    ptr, idx, val = graph_on(gpu, *heavy_graph())
+    plan = mk.get_plan(ptr, idx, val, ptr.numel() - 1, idx.numel(), 256, 16)
+    info = plan.info()
+    assert info["fwd_split_rows"] == 2
+    assert info["bwd_blocks"] * info["bwd_block_cols"] >= ptr.numel() - 1
+    assert info["fwd_tasks"] > 0 and info["bwd_tasks"] >= info["bwd_blocks"]
+
+
+# ------------------------------------------------------------------------ autograd
+def test_autograd_matches_dense_torch(gpu):
+    p, ix, v = GRAPHS["synthetic"]()
+    n = p.size - 1
+    d, k = 64, 16
+    x = graphs.features(n, d, seed=8).double()
+    w = graphs.features(n, d, seed=9).double()
+    graph = mk.CSRGraph(*graph_on(gpu, p, ix, v))
+    xg = x.float().to(gpu).requires_grad_(True)
+    y = mk.maxk_aggregate(xg, graph, k)
+    loss = (y.double() * w.to(gpu)).sum()
+    loss.backward()
+    # dense float64 reference: topk mask -> A @ (x*mask)
+    xr = x.clone().requires_grad_(True)
+    idx_t = torch.topk(xr.detach(), k, dim=1).indices
+    mask = torch.zeros_like(xr).scatter_(1, idx_t, 1.0)
+    a = torch.sparse_csr_tensor(torch.from_numpy(p).long(), torch.from_numpy(ix).long(),
+                                torch.from_numpy(v).double(), size=(n, n)).to_dense()
+    yr = a @ (xr * mask)
+    (yr * w).sum().backward()
+    assert torch.allclose(y.double().cpu(), yr.detach(), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(xg.grad.double().cpu(), xr.grad, rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------------ dense comparator
+def test_dense_spmm_vs_oracle(gpu):
+    p, ix, v = GRAPHS["heavy_split"]()
+    n = p.size - 1
+    x = graphs.features(n, 64, seed=2)
+    ref = oracle.dense_spmm(p, ix, v, x.numpy())          # f32 sums (DGL semantics)
+    mag = oracle.dense_spmm(p, ix, np.abs(v), np.abs(x.numpy()))
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    y = mk.dense_spmm(ptr, idx, val, x.to(gpu))
+    # both sides accumulate in f32 in different orders: bound by the summed magnitude
+    assert_close(y, ref, mag, rtol=2e-6 * 64)
