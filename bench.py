@@ -1,0 +1,309 @@
+#!/usr/bin/env python3
+"""Benchmark: SpGEMM forward + SSpMM backward edges/s on Reddit (synthetic, D=256, k=16).
+
+Metric (BASELINE.json): "SpGEMM+SSpMM edges/sec on Reddit, hidden=256, k in {8,16,32,64};
+%HBM roofline". One step = one SpGEMM forward over all E edges + one SSpMM backward over
+all E edges, inputs (graph, CBSR features, upstream gradient) resident in HBM;
+value = 2E / step time (edges/s = 2E / (t_fwd + t_bwd)).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+N > 1: the rows are partitioned over the ranks (strong scaling: the Reddit graph is fixed)
+and each step includes the RCCL all-gather of the CBSR block and the reduce-scatter of
+grad_sp (maxk_kernels.dist). Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "spgemm-gnn_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import maxk_kernels as mk  # noqa: E402
+from maxk_kernels import graphs  # noqa: E402
+from maxk_kernels.dist import RowPartition, ShardedAggregation  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def fwd_bytes(n, e, k, d):
+    """Algorithmic (compulsory) bytes of one SpGEMM forward."""
+    return 4 * (n + 1) + 8 * e + 5 * k * n + 4 * d * n
+
+
+def bwd_bytes(n, e, k, d):
+    """Algorithmic bytes of one SSpMM backward: rowptr, idx+val, G, selector, grad write."""
+    return 4 * (n + 1) + 8 * e + 4 * d * n + k * n + 4 * k * n
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def event_time_ms(fn, reps):
+    """Average device time of fn() over reps launches, HIP events on the current stream
+    (the C ABI launches on torch's current stream)."""
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d, sample_frac, reps, log_fn):
+    """DGL-semantics dense CSR SpMM on the host cores (oracle C/OpenMP restatement of
+    update_all(copy_u, sum) with edge weights; the dense MaxK output as DGL sees it),
+    forward A @ X and backward A^T @ G, on a bounded sample of the destination rows."""
+    from oracle import oracle
+
+    n = ptr.numel() - 1
+    dev = ptr.device
+    # dense MaxK output and the transposed graph, built on the GPU, copied to the host
+    x = torch.zeros((n, d), dtype=torch.float32, device=dev)
+    x.scatter_(1, sp_index.long(), sp_data)
+    order = torch.argsort(idx.long(), stable=True)
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), (ptr[1:] - ptr[:-1]).long())
+    idx_t = rows[order].to(torch.int32)
+    val_t = val[order]
+    cnt = torch.bincount(idx.long(), minlength=n)
+    ptr_t = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    ptr_t[1:] = torch.cumsum(cnt, 0)
+    h = {k: v.cpu().numpy() for k, v in dict(ptr=ptr, idx=idx, val=val, x=x, g=g,
+                                                ptr_t=ptr_t.to(torch.int32), idx_t=idx_t,
+                                                val_t=val_t).items()}
+    del x, order, rows, idx_t, val_t, cnt, ptr_t
+    e = int(h["ptr"][-1])
+    target = int(e * sample_frac)
+    r_f = int(np.searchsorted(h["ptr"], target))
+    r_b = int(np.searchsorted(h["ptr_t"], target))
+    y = np.zeros((n, d), np.float32)
+    # warm-up on a small slice (page-in), then the timed sample
+    oracle.dense_spmm(h["ptr"], h["idx"], h["val"], h["x"], row_end=min(n, 2000), out=y)
+    tf = tb = 0.0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        oracle.dense_spmm(h["ptr"], h["idx"], h["val"], h["x"], row_end=r_f, out=y)
+        t1 = time.perf_counter()
+        oracle.dense_spmm(h["ptr_t"], h["idx_t"], h["val_t"], h["g"], row_end=r_b, out=y)
+        t2 = time.perf_counter()
+        tf += t1 - t0
+        tb += t2 - t1
+    e_f, e_b = int(h["ptr"][r_f]), int(h["ptr_t"][r_b])
+    log_fn(f"cpu baseline: {reps}x fwd {e_f} edges in {tf:.2f}s, bwd {e_b} edges in {tb:.2f}s")
+    return {
+        "value": reps * (e_f + e_b) / (tf + tb),
+        "unit": "edges/s",
+        "cores": oracle.num_threads(),
+        "kind": "port",
+        "sample": (f"DGL-semantics dense CSR SpMM (oracle C/OpenMP, f32): forward A@X over "
+                   f"rows [0,{r_f}) = {e_f} edges and backward A^T@G over rows [0,{r_b}) of "
+                   f"the transposed graph = {e_b} edges ({sample_frac:.0%} of E each), "
+                   f"D={d}, X = dense MaxK output, {reps} repetitions"),
+        "fwd_s": tf / reps,
+        "bwd_s": tb / reps,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--dataset", default="reddit", choices=sorted(graphs.DATASETS))
+    ap.add_argument("--k", type=int, default=16)
+    ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--cpu-sample", type=float, default=1.0,
+                    help="fraction of E timed per direction for the CPU baseline")
+    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-comparator", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n, e_target = graphs.DATASETS[args.dataset]
+    d, k = args.dim, args.k
+    t0 = time.perf_counter()
+    ptr, idx = graphs.synthetic_csr(n, e_target, seed=97, device=dev)
+    val = graphs.sage_mean_values(ptr)
+    e = idx.numel()
+    torch.cuda.synchronize()
+    log(f"graph {args.dataset}: N={n} E={e} generated in {time.perf_counter() - t0:.1f}s")
+
+    part = RowPartition(ptr, world)
+    r0, r1 = part.rows(rank)
+    h = graphs.features(n, d, seed=97, device=dev)[r0:r1].contiguous()
+    g = graphs.features(n, d, seed=98, device=dev)[r0:r1].contiguous()
+    sp_data, sp_index = mk.maxk_forward(h, k, return_index=True)
+
+    t0 = time.perf_counter()
+    if world == 1:
+        plan = mk.get_plan(ptr, idx, val, n, e, d, k)
+        info = plan.info()
+        out = torch.empty((n, d), dtype=torch.float32, device=dev)
+        grad_sp = torch.empty((n, k), dtype=torch.float32, device=dev)
+
+        def fwd():
+            plan.forward(sp_data, sp_index, out)
+
+        def bwd():
+            plan.backward(g, sp_index, grad_sp)
+
+        def step():
+            fwd()
+            bwd()
+    else:
+        shard = ShardedAggregation(part, rank, ptr, idx, val, d, k)
+        plan = shard.plan
+        info = plan.info()
+        out = torch.empty((r1 - r0, d), dtype=torch.float32, device=dev)
+        grad_sp = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
+        shard.gather(sp_data, sp_index)
+
+        def fwd():
+            plan.forward(shard.table_data, shard.table_index, out)
+
+        def bwd():
+            plan.backward(g, shard.table_index, grad_sp)
+
+        def step():
+            shard.forward(sp_data, sp_index)
+            shard.backward(g)
+    torch.cuda.synchronize()
+    plan_s = time.perf_counter() - t0
+    log(f"plan built in {plan_s:.2f}s: {info}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = 2.0 * e / (elapsed / args.steps)
+
+    # per-kernel device time (HIP events on the launch stream), this rank's shard
+    reps = max(5, args.steps)
+    fwd_ms = event_time_ms(fwd, reps)
+    bwd_ms = event_time_ms(bwd, reps)
+    e_loc = info["num_edges"]
+    n_loc = info["num_nodes"]
+    fb = fwd_bytes(n_loc, e_loc, k, d)
+    bb = bwd_bytes(n_loc, e_loc, k, d)
+    fwd_gbs = fb / (fwd_ms * 1e-3) / 1e9
+    bwd_gbs = bb / (bwd_ms * 1e-3) / 1e9
+    dom = "sspmm_bwd" if bwd_ms >= fwd_ms else "spgemm_fwd"
+    achieved = bwd_gbs if dom == "sspmm_bwd" else fwd_gbs
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            key = f"{args.dataset}:k{k}:d{d}:n{world}"
+            traffic = tj.get(key, {}).get(dom)
+        except (OSError, ValueError):
+            traffic = None
+
+    result = {
+        "metric": "SpGEMM+SSpMM edges/sec on Reddit, hidden=256, k=16; %HBM roofline",
+        "value": value,
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Reddit-shaped graph: lognormal degrees sigma=1.2, uniform "
+                "columns, self-loops, seed 97; N(0,1) features seed 97, upstream grad seed 98)",
+        "config": {
+            "workload": f"{args.dataset} SpGEMM fwd + SSpMM bwd over CBSR (MaxK exact), "
+                        f"D={d}, k={k}",
+            "dataset": args.dataset, "num_nodes": n, "num_edges": e, "dim_origin": d,
+            "dim_k": k,
+            "parallelism": "single-gpu" if world == 1 else
+            f"row-partition x{world} + RCCL all-gather(CBSR) / reduce-scatter(grad_sp)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes": bb if dom == "sspmm_bwd" else fb,
+        },
+        "fwd_ms": fwd_ms,
+        "bwd_ms": bwd_ms,
+        "fwd_edges_per_s": e_loc / (fwd_ms * 1e-3),
+        "bwd_edges_per_s": e_loc / (bwd_ms * 1e-3),
+        "fwd_roofline_frac": fwd_gbs / HBM_PEAK_GBS,
+        "bwd_roofline_frac": bwd_gbs / HBM_PEAK_GBS,
+        "plan_build_s": plan_s,
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_comparator:
+        # rocSPARSE CSR SpMM on the dense MaxK output (the reference's cuSPARSE comparator,
+        # spmm_cusparse SO@0x243a0), through torch.sparse on ROCm
+        try:
+            x = torch.zeros((n, d), dtype=torch.float32, device=dev)
+            x.scatter_(1, sp_index.long(), sp_data)
+            a = torch.sparse_csr_tensor(ptr.long(), idx.long(), val, size=(n, n))
+            sp_ms = event_time_ms(lambda: torch.sparse.mm(a, x), 5)
+            result["comparator"] = {
+                "rocsparse_spmm_dense_ms": sp_ms,
+                "spgemm_fwd_speedup_vs_rocsparse": sp_ms / fwd_ms,
+            }
+            del x, a
+        except Exception as exc:  # pragma: no cover - depends on torch build
+            result["comparator"] = {"error": repr(exc)[:200]}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d,
+                                              args.cpu_sample, args.cpu_reps, log)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,9 @@ constexpr int kFwdTileRows = 16;        // destination rows per forward work-gro
 constexpr int kFwdThreads = 256;        // 4 waves
 constexpr int kBwdThreads = 512;        // 8 waves
 constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
+constexpr int kFwdUnroll = 8;           // independent sub-steps in flight per wave
+constexpr int kBwdUnroll = 8;
+constexpr int kBwdLdsBudget = 150 * 1024; // one 512-thread work-group per CU
 
 // Thread-local error message plumbing for maxk_last_error().
 void set_error(const std::string& msg);
@@ -56,9 +59,9 @@ struct FwdTask {
 };
 static_assert(sizeof(FwdTask) == 16, "FwdTask is loaded as one dwordx4");
 
-// Backward work item: edges [e0, e1) of the column-block-major edge list, all with
-// source column in [col0, col0 + ncols). shared != 0: more than one work-group owns
-// the block, so the LDS accumulator is flushed with float atomics into a pre-zeroed
+// Backward work item: edges [e0, e1) of the column-block-major, row-sorted edge list, all
+// with source column in [col0, col0 + ncols). shared != 0: the block is split over several
+// work-groups, so its LDS accumulator is flushed with float atomics into a pre-zeroed
 // grad_sp; otherwise it is stored.
 struct BwdTask {
   int32_t col0;
@@ -70,8 +73,23 @@ struct BwdTask {
 };
 static_assert(sizeof(BwdTask) == 32, "BwdTask is 2 x dwordx4");
 
+__host__ __device__ inline int bwd_feats(int k) { return (k % 4 == 0) ? 4 : 1; }
+__host__ __device__ inline int bwd_lanes(int k) {
+  return bwd_feats(k) == 4 ? k / 4 : (k < kWave ? k : kWave);
+}
+__host__ __device__ inline int bwd_slots_per_wave(int k) {
+  const int s = kWave / bwd_lanes(k);
+  return s < 16 ? s : 16;
+}
+
 __device__ __forceinline__ void lds_add(float* p, float v) {
-  // Lowers to ds_add_f32 (no return) for an LDS address.
+  // Lowers to ds_add_f32 (no return) for an LDS address. NOTE: ~30x slower than integer
+  // LDS atomics on gfx950 (tools/ubench_atomics); kept off the hot paths.
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void lds_add(double* p, double v) {
+  // ds_add_f64 (no return).
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -84,7 +102,8 @@ __device__ __forceinline__ void global_add(float* p, float v) {
 
 // Opaque plan (definition shared by plan.hip and the kernels' launchers).
 struct maxk_plan {
-  int32_t num_nodes = 0;
+  int32_t num_nodes = 0;   // destination rows
+  int32_t num_cols = 0;    // source columns (rows of the CBSR tables / grad_sp)
   int64_t num_edges = 0;
   int32_t dim_origin = 0;
   int32_t dim_k = 0;
@@ -101,8 +120,8 @@ struct maxk_plan {
   maxk::BwdTask* bwd_tasks = nullptr;
   int32_t n_bwd_tasks = 0;
   int32_t n_bwd_shared = 0;
-  int32_t* bwd_perm = nullptr;   // CSR edge id of each block-major edge
-  int32_t* bwd_row = nullptr;    // destination row r of each block-major edge
+  int32_t* bwd_perm = nullptr;   // CSR edge id of each reordered edge
+  int32_t* bwd_row = nullptr;    // destination row r of each reordered edge
   int32_t* bwd_col = nullptr;    // source column c
   float* bwd_val = nullptr;      // val snapshot
   int64_t device_bytes = 0;

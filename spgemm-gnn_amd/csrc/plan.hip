@@ -24,7 +24,6 @@ namespace maxk {
 
 size_t bwd_lds_bytes(int block_cols, int k);
 
-constexpr size_t kBwdLdsBudget = 64 * 1024;  // two 512-thread work-groups per CU
 
 __global__ void expand_rows_kernel(const int32_t* __restrict__ ptr, int N,
                                    int32_t* __restrict__ row_of) {
@@ -35,16 +34,18 @@ __global__ void expand_rows_kernel(const int32_t* __restrict__ ptr, int N,
   for (int e = ptr[row] + lane; e < e1; e += kWave) row_of[e] = row;
 }
 
-// Also validates the column ids: any idx outside [0, N) sets *bad (the compute kernels
-// index the CBSR tables with idx and must never read outside them).
-__global__ void block_key_kernel(const int32_t* __restrict__ idx, int64_t E, int C, int N,
-                                 uint32_t* __restrict__ keys, int32_t* __restrict__ ids,
-                                 int* __restrict__ bad) {
+// Sort key of each edge for the backward: its source-column block c / C (a stable radix
+// sort then yields the block-major, destination-row-sorted edge list). Also validates the
+// column ids: any idx outside [0, NC) sets *bad (the compute kernels index the CBSR tables
+// with idx and must never read outside them).
+__global__ void bwd_key_kernel(const int32_t* __restrict__ idx, int64_t E, int C, int NC,
+                               uint32_t* __restrict__ keys, int32_t* __restrict__ ids,
+                               int* __restrict__ bad) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int c = idx[e];
-    if (c < 0 || c >= N) atomicOr(bad, 1);
-    const int cc = c < 0 ? 0 : (c >= N ? N - 1 : c);
+    if (c < 0 || c >= NC) atomicOr(bad, 1);
+    const int cc = c < 0 ? 0 : (c >= NC ? NC - 1 : c);
     keys[e] = (uint32_t)(cc / C);
     ids[e] = (int32_t)e;
   }
@@ -65,17 +66,17 @@ __global__ void gather_bwd_kernel(const int32_t* __restrict__ perm,
   }
 }
 
-// offs[b] = first position j with skeys[j] >= b, b in [0, nblocks].
-__global__ void block_offsets_kernel(const uint32_t* __restrict__ skeys, int64_t E,
-                                     int nblocks, int64_t* __restrict__ offs) {
+// offs[b] = first position j with skeys[j] >= b, b in [0, nkeys].
+__global__ void key_offsets_kernel(const uint32_t* __restrict__ skeys, int64_t E, int nkeys,
+                                   int32_t* __restrict__ offs) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > nblocks) return;
+  if (b > nkeys) return;
   int64_t lo = 0, hi = E;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
     if (skeys[mid] < (uint32_t)b) lo = mid + 1; else hi = mid;
   }
-  offs[b] = lo;
+  offs[b] = (int32_t)lo;
 }
 
 static void dfree(void* q) { if (q) (void)hipFree(q); }
@@ -142,8 +143,15 @@ using namespace maxk;
 extern "C" int maxk_plan_create(const int32_t* ptr, const int32_t* idx, const float* val,
                                 int32_t N, int64_t E, int32_t D, int32_t k, void* stream,
                                 maxk_plan** out_plan) {
+  return maxk_plan_create_rect(ptr, idx, val, N, N, E, D, k, stream, out_plan);
+}
+
+extern "C" int maxk_plan_create_rect(const int32_t* ptr, const int32_t* idx, const float* val,
+                                     int32_t N, int32_t NC, int64_t E, int32_t D, int32_t k,
+                                     void* stream, maxk_plan** out_plan) {
   MAXK_CHECK_ARG(out_plan != nullptr, "maxk_plan_create: out_plan is null");
   *out_plan = nullptr;
+  MAXK_CHECK_ARG(NC >= 0 && (E == 0 || NC > 0), "maxk_plan_create: num_cols out of range");
   MAXK_CHECK_ARG(N >= 0 && E >= 0 && E < (int64_t)INT32_MAX,
                  "maxk_plan_create: sizes out of range (E must fit int32)");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_plan_create: dim_origin must be in [1, 256]");
@@ -153,6 +161,7 @@ extern "C" int maxk_plan_create(const int32_t* ptr, const int32_t* idx, const fl
 
   maxk_plan* p = new maxk_plan();
   p->num_nodes = N;
+  p->num_cols = NC;
   p->num_edges = E;
   p->dim_origin = D;
   p->dim_k = k;
@@ -219,10 +228,21 @@ extern "C" int maxk_plan_create(const int32_t* ptr, const int32_t* idx, const fl
   }
 
   // ---------------- backward
-  const size_t per_col = bwd_lds_bytes(1, k);
-  int C = (int)std::max<size_t>(1, kBwdLdsBudget / per_col);
-  C = std::min(C, std::max(N, 1));
-  const int nblocks = N > 0 ? (N + C - 1) / C : 0;
+  // Column blocks of C columns (k f64 accumulators each, <= kBwdLdsBudget of LDS: one
+  // 512-thread work-group per CU); each block's edge range is cut into chunks so that about
+  // 2 x CUs work-groups exist; blocks with several chunks flush with float atomics.
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        cus = prop.multiProcessorCount;
+    }
+  }
+  int C = std::max(1, kBwdLdsBudget / (k * (int)sizeof(double)));
+  C = std::min(C, std::max(NC, 1));
+  const int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
   p->bwd_block_cols = C;
   p->n_bwd_blocks = nblocks;
   std::vector<int64_t> offs(nblocks + 1, 0);
@@ -232,14 +252,14 @@ extern "C" int maxk_plan_create(const int32_t* ptr, const int32_t* idx, const fl
     PLAN_TRY(hipMalloc(&keys_out, sizeof(uint32_t) * E));
     PLAN_TRY(hipMalloc(&ids_in, sizeof(int32_t) * E));
     PLAN_TRY(hipMalloc(&p->bwd_perm, sizeof(int32_t) * E));
-    hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
     PLAN_TRY(hipMalloc(&d_bad, sizeof(int)));
     PLAN_TRY(hipMemsetAsync(d_bad, 0, sizeof(int), s));
-    hipLaunchKernelGGL(block_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, E, C, N,
+    hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
+    hipLaunchKernelGGL(bwd_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, E, C, NC,
                        keys_in, ids_in, d_bad);
     PLAN_TRY(hipGetLastError());
     int end_bit = 1;
-    while ((1 << end_bit) < nblocks) ++end_bit;
+    while ((1ll << end_bit) < (long long)nblocks) ++end_bit;
     size_t temp_bytes = 0;
     PLAN_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, ids_in,
                                                 p->bwd_perm, (int)E, 0, end_bit, s));
@@ -252,44 +272,35 @@ extern "C" int maxk_plan_create(const int32_t* ptr, const int32_t* idx, const fl
     p->device_bytes += (int64_t)E * 16;
     hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
                        p->bwd_perm, row_of, idx, val, E, p->bwd_row, p->bwd_col, p->bwd_val);
-    PLAN_TRY(hipMalloc(&d_offs, sizeof(int64_t) * (nblocks + 1)));
-    hipLaunchKernelGGL(block_offsets_kernel, dim3((nblocks + 256) / 256), dim3(256), 0, s,
-                       keys_out, E, nblocks, d_offs);
+    PLAN_TRY(hipMalloc(&d_offs, sizeof(int32_t) * (nblocks + 1)));
+    hipLaunchKernelGGL(key_offsets_kernel, dim3(nblocks / 256 + 1), dim3(256), 0, s, keys_out,
+                       E, nblocks, reinterpret_cast<int32_t*>(d_offs));
     PLAN_TRY(hipGetLastError());
-    PLAN_TRY(hipMemcpyAsync(offs.data(), d_offs, sizeof(int64_t) * (nblocks + 1),
+    std::vector<int32_t> offs32(nblocks + 1);
+    PLAN_TRY(hipMemcpyAsync(offs32.data(), d_offs, sizeof(int32_t) * (nblocks + 1),
                             hipMemcpyDeviceToHost, s));
     int bad = 0;
     PLAN_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
     PLAN_TRY(hipStreamSynchronize(s));
     if (bad) {
-      set_error("maxk_plan_create: idx contains column ids outside [0, num_nodes)");
+      set_error("maxk_plan_create: idx contains column ids outside [0, num_cols)");
       return fail(MAXK_ERR_INVALID_ARG);
     }
+    for (int b = 0; b <= nblocks; ++b) offs[b] = offs32[b];
   }
-  int cus = 256;
-  {
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess) {
-      hipDeviceProp_t prop;
-      if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
-        cus = prop.multiProcessorCount;
-    }
-  }
-  const int64_t desired = (int64_t)cus * 4;
-  const int64_t bcap = std::max<int64_t>(4096, (E + desired - 1) / std::max<int64_t>(desired, 1));
+  const int64_t target_tasks = 2 * (int64_t)cus;
+  const int chunks = (int)std::max<int64_t>(1, (target_tasks + nblocks - 1) / std::max(nblocks, 1));
   std::vector<BwdTask> btasks;
   int nshared = 0;
   for (int b = 0; b < nblocks; ++b) {
     const int64_t o0 = offs[b], o1 = offs[b + 1];
     const int64_t nnz = o1 - o0;
-    const int nch = (int)std::max<int64_t>(1, (nnz + bcap - 1) / bcap);
-    const int col0 = b * C;
-    const int ncols = std::min(C, N - col0);
+    const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, nnz / 1024));
     if (nch > 1) ++nshared;
     for (int i = 0; i < nch; ++i) {
       BwdTask t{};
-      t.col0 = col0;
-      t.ncols = ncols;
+      t.col0 = b * C;
+      t.ncols = std::min(C, NC - t.col0);
       t.e0 = (int32_t)(o0 + nnz * i / nch);
       t.e1 = (int32_t)(o0 + nnz * (i + 1) / nch);
       t.shared = nch > 1;
@@ -333,6 +344,7 @@ extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* st
 extern "C" int maxk_plan_get_info(const maxk_plan* p, maxk_plan_info* info) {
   MAXK_CHECK_ARG(p != nullptr && info != nullptr, "maxk_plan_get_info: null pointer");
   info->num_nodes = p->num_nodes;
+  info->num_cols = p->num_cols;
   info->num_edges = p->num_edges;
   info->dim_origin = p->dim_origin;
   info->dim_k = p->dim_k;

@@ -32,19 +32,18 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
     float* __restrict__ out, int D, int k) {
-  extern __shared__ __align__(16) float smem[];
+  // f64 LDS accumulators: on gfx950 ds_add_f64 sustains ~9x the rate of ds_add_f32
+  // (tools/ubench_atomics: 1.85e12 vs 2.0e11 adds/s chip-wide), and f64 sums make the
+  // f32 result independent of the atomic arrival order in all but pathological cases.
+  extern __shared__ __align__(16) double smem_d[];
   const FwdTask t = tasks[blockIdx.x];
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
-  float* acc = smem;
-  int* sptr = reinterpret_cast<int*>(smem + kFwdTileRows * D);
+  double* acc = smem_d;
+  int* sptr = reinterpret_cast<int*>(smem_d + kFwdTileRows * D);
   const int n = nrows * D;
-  if ((D & 3) == 0) {
-    for (int i = threadIdx.x * 4; i < n; i += kFwdThreads * 4)
-      *reinterpret_cast<float4*>(acc + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-  } else {
-    for (int i = threadIdx.x; i < n; i += kFwdThreads) acc[i] = 0.f;
-  }
+  for (int i = threadIdx.x * 2; i < n; i += kFwdThreads * 2)
+    *reinterpret_cast<double2*>(acc + i) = make_double2(0.0, 0.0);
   for (int i = threadIdx.x; i <= nrows; i += kFwdThreads)
     sptr[i] = split ? (i == 0 ? t.e0 : t.e1) : ptr[t.row0 + i];
   __syncthreads();
@@ -60,28 +59,66 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   const bool lane_on = slot < EPS;
   constexpr int kWaves = kFwdThreads / kWave;
 
-  for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
-    const int e = base + slot;
-    if (lane_on && e < t.e1) {
-      int lo = 0, hi = nrows - 1;  // row of e: last j with sptr[j] <= e
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (sptr[mid] <= e) lo = mid; else hi = mid - 1;
+  if constexpr (VEC == 4) {
+    // U sub-steps per iteration with every load issued before the first LDS update: the
+    // chain idx/val -> CBSR row -> LDS has two dependent global round trips, so memory-
+    // level parallelism comes from U independent sub-steps per wave. Out-of-range lanes
+    // load a clamped (valid) edge and skip the update.
+    constexpr int U = kFwdUnroll;
+    const int last = t.e1 - 1;
+    for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
+      int c[U], rl[U];
+      float v[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = base + u * EPS + slot;
+        ok[u] = lane_on && e < t.e1;
+        const int ec = ok[u] ? e : last;
+        c[u] = idx[ec];
+        v[u] = val[ec];
+        int lo = 0, hi = nrows - 1;  // row of ec: last j with sptr[j] <= ec
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (sptr[mid] <= ec) lo = mid; else hi = mid - 1;
+        }
+        rl[u] = lo;
       }
-      const int c = idx[e];
-      const float v = val[e];
-      float* arow = acc + lo * D;
-      const size_t off = (size_t)c * k + l0;
-      if constexpr (VEC == 4) {
-        const float4 x = *reinterpret_cast<const float4*>(sp_data + off);
-        const uint32_t s = *reinterpret_cast<const uint32_t*>(sp_index + off);
-        lds_add(arow + (s & 0xffu), v * x.x);
-        lds_add(arow + ((s >> 8) & 0xffu), v * x.y);
-        lds_add(arow + ((s >> 16) & 0xffu), v * x.z);
-        lds_add(arow + (s >> 24), v * x.w);
-      } else {
+      float4 x[U];
+      uint32_t sel[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t off = (size_t)c[u] * k + l0;
+        x[u] = *reinterpret_cast<const float4*>(sp_data + off);
+        sel[u] = *reinterpret_cast<const uint32_t*>(sp_index + off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ok[u]) {
+          double* arow = acc + rl[u] * D;
+          const uint32_t sv = sel[u];
+          lds_add(arow + (sv & 0xffu), (double)(v[u] * x[u].x));
+          lds_add(arow + ((sv >> 8) & 0xffu), (double)(v[u] * x[u].y));
+          lds_add(arow + ((sv >> 16) & 0xffu), (double)(v[u] * x[u].z));
+          lds_add(arow + (sv >> 24), (double)(v[u] * x[u].w));
+        }
+      }
+    }
+  } else {
+    for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
+      const int e = base + slot;
+      if (lane_on && e < t.e1) {
+        int lo = 0, hi = nrows - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (sptr[mid] <= e) lo = mid; else hi = mid - 1;
+        }
+        const int c = idx[e];
+        const float v = val[e];
+        double* arow = acc + lo * D;
         const size_t rb = (size_t)c * k;
-        for (int l = l0; l < k; l += L) lds_add(arow + sp_index[rb + l], v * sp_data[rb + l]);
+        for (int l = l0; l < k; l += L)
+          lds_add(arow + sp_index[rb + l], (double)(v * sp_data[rb + l]));
       }
     }
   }
@@ -90,13 +127,17 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   float* dst = out + (size_t)t.row0 * D;
   if (!split) {
     if ((D & 3) == 0) {
-      for (int i = threadIdx.x * 4; i < n; i += kFwdThreads * 4)
-        *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(acc + i);
+      for (int i = threadIdx.x * 4; i < n; i += kFwdThreads * 4) {
+        const double2 a = *reinterpret_cast<const double2*>(acc + i);
+        const double2 b = *reinterpret_cast<const double2*>(acc + i + 2);
+        *reinterpret_cast<float4*>(dst + i) =
+            make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
+      }
     } else {
-      for (int i = threadIdx.x; i < n; i += kFwdThreads) dst[i] = acc[i];
+      for (int i = threadIdx.x; i < n; i += kFwdThreads) dst[i] = (float)acc[i];
     }
   } else {
-    for (int i = threadIdx.x; i < D; i += kFwdThreads) global_add(dst + i, acc[i]);
+    for (int i = threadIdx.x; i < D; i += kFwdThreads) global_add(dst + i, (float)acc[i]);
   }
 }
 
@@ -111,29 +152,23 @@ __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, fl
 // --------------------------------------------------------------------------------------
 // backward
 // --------------------------------------------------------------------------------------
-// LDS layout of a column's k accumulators: feature l = VEC*q + i lives at
-// i*(k/VEC) + q, and columns are KS = k (+VEC when k/VEC is even) floats apart, so the
-// L lanes of one edge hit consecutive banks and neighbouring columns start on different
-// bank groups.
-__host__ __device__ inline int bwd_col_stride(int k, int vec) {
-  const int L = k / vec;
-  return (vec > 1 && (L % 2) == 0) ? k + vec : k;
-}
-
-template <int VEC>
+// Flat edge processing in (column block, destination row) order: the edges one wave
+// instruction covers share few rows of grad_out, so its gathers stay in the CU's L1.
+// Accumulation: f64 LDS atomics (ds_add_f64 ~9x the ds_add_f32 rate on gfx950; any wave
+// may update any column of the block, which is what keeps the row locality).
+template <int F>
 __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
     const BwdTask* __restrict__ tasks, const int32_t* __restrict__ erow,
     const int32_t* __restrict__ ecol, const float* __restrict__ evals,
     const float* __restrict__ G, const uint8_t* __restrict__ sp_index,
     float* __restrict__ grad_sp, int D, int k) {
-  extern __shared__ __align__(16) float acc[];
+  extern __shared__ __align__(16) double bacc[];  // [ncols][k]
   const BwdTask t = tasks[blockIdx.x];
-  const int KS = bwd_col_stride(k, VEC);
-  const int L = (VEC == 4) ? k / 4 : (k < kWave ? k : kWave);
-  const int nacc = t.ncols * KS;
-  for (int i = threadIdx.x; i < nacc; i += kBwdThreads) acc[i] = 0.f;
+  const int n = t.ncols * k;
+  for (int i = threadIdx.x; i < n; i += kBwdThreads) bacc[i] = 0.0;
   __syncthreads();
 
+  const int L = bwd_lanes(k);
   const int EPS = kWave / L;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
@@ -141,42 +176,65 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
   const int q = lane - slot * L;
   const bool lane_on = slot < EPS;
   constexpr int kWaves = kBwdThreads / kWave;
+  constexpr int U = kBwdUnroll;
+  const int last = t.e1 - 1;
 
-  for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
-    const int e = base + slot;
-    if (lane_on && e < t.e1) {
-      const int r = erow[e];
-      const int c = ecol[e];
-      const float v = evals[e];
-      const float* grow = G + (size_t)r * D;
-      float* a = acc + (c - t.col0) * KS + q;
-      const size_t off = (size_t)c * k + (size_t)q * VEC;
-      if constexpr (VEC == 4) {
-        const uint32_t s = *reinterpret_cast<const uint32_t*>(sp_index + off);
-        const float g0 = grow[s & 0xffu];
-        const float g1 = grow[(s >> 8) & 0xffu];
-        const float g2 = grow[(s >> 16) & 0xffu];
-        const float g3 = grow[s >> 24];
-        lds_add(a, v * g0);
-        lds_add(a + L, v * g1);
-        lds_add(a + 2 * L, v * g2);
-        lds_add(a + 3 * L, v * g3);
-      } else {
-        const size_t rb = (size_t)c * k;
-        for (int l = q; l < k; l += L) lds_add(a + (l - q), v * grow[sp_index[rb + l]]);
+  for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
+    int r[U], c[U];
+    float v[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * EPS + slot;
+      ok[u] = lane_on && e < t.e1;
+      const int ec = ok[u] ? e : last;
+      r[u] = erow[ec];
+      c[u] = ecol[ec];
+      v[u] = evals[ec];
+    }
+    if constexpr (F == 4) {
+      uint32_t sel[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        sel[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)c[u] * k + q * 4);
+      float g[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float* grow = G + (size_t)r[u] * D;
+        g[u][0] = grow[sel[u] & 0xffu];
+        g[u][1] = grow[(sel[u] >> 8) & 0xffu];
+        g[u][2] = grow[(sel[u] >> 16) & 0xffu];
+        g[u][3] = grow[sel[u] >> 24];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ok[u]) {
+          double* a = bacc + (c[u] - t.col0) * k + q * 4;
+          lds_add(a, (double)(v[u] * g[u][0]));
+          lds_add(a + 1, (double)(v[u] * g[u][1]));
+          lds_add(a + 2, (double)(v[u] * g[u][2]));
+          lds_add(a + 3, (double)(v[u] * g[u][3]));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ok[u]) {
+          const float* grow = G + (size_t)r[u] * D;
+          const uint8_t* srow = sp_index + (size_t)c[u] * k;
+          double* a = bacc + (c[u] - t.col0) * k;
+          for (int l = q; l < k; l += L) lds_add(a + l, (double)(v[u] * grow[srow[l]]));
+        }
       }
     }
   }
   __syncthreads();
 
   float* dst = grad_sp + (size_t)t.col0 * k;
-  const int n = t.ncols * k;
-  for (int i = threadIdx.x; i < n; i += kBwdThreads) {
-    const int cl = i / k;
-    const int l = i - cl * k;
-    const int pos = (VEC == 4) ? cl * KS + (l & 3) * L + (l >> 2) : cl * KS + l;
-    if (t.shared) global_add(dst + i, acc[pos]);
-    else dst[i] = acc[pos];
+  if (t.shared) {
+    for (int i = threadIdx.x; i < n; i += kBwdThreads) global_add(dst + i, (float)bacc[i]);
+  } else {
+    for (int i = threadIdx.x; i < n; i += kBwdThreads) dst[i] = (float)bacc[i];
   }
 }
 
@@ -206,13 +264,10 @@ __global__ __launch_bounds__(256) void dense_spmm_kernel(
 }
 
 static size_t fwd_lds_bytes(int D) {
-  return (size_t)kFwdTileRows * D * sizeof(float) + (kFwdTileRows + 1) * sizeof(int);
+  return (size_t)kFwdTileRows * D * sizeof(double) + (kFwdTileRows + 1) * sizeof(int);
 }
 
-size_t bwd_lds_bytes(int block_cols, int k) {
-  const int vec = (k % 4 == 0) ? 4 : 1;
-  return (size_t)block_cols * bwd_col_stride(k, vec) * sizeof(float);
-}
+size_t bwd_lds_bytes(int block_cols, int k) { return (size_t)block_cols * k * sizeof(double); }
 
 }  // namespace maxk
 
@@ -273,9 +328,18 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   MAXK_CHECK_ARG(grad_out && sp_index && grad_sp, "maxk_sspmm_backward: null pointer");
   hipStream_t s = (hipStream_t)stream;
   if (plan->n_bwd_shared > 0)
-    MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)N * k * sizeof(float), s));
+    MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)plan->num_cols * k * sizeof(float), s));
   const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k);
-  if (k % 4 == 0)
+  if (plan->n_bwd_tasks == 0) return MAXK_OK;
+  static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB/CU)
+  if (!attr_set) {
+    MAXK_HIP_TRY(hipFuncSetAttribute((const void*)sspmm_bwd_kernel<4>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLdsBudget));
+    MAXK_HIP_TRY(hipFuncSetAttribute((const void*)sspmm_bwd_kernel<1>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLdsBudget));
+    attr_set = true;
+  }
+  if (bwd_feats(k) == 4)
     hipLaunchKernelGGL(sspmm_bwd_kernel<4>, dim3(plan->n_bwd_tasks), dim3(kBwdThreads), lds, s,
                        plan->bwd_tasks, plan->bwd_row, plan->bwd_col, plan->bwd_val, grad_out,
                        sp_index, grad_sp, D, k);

@@ -27,6 +27,8 @@ SIGNATURES = {
     "maxk_scatter_backward": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "maxk_plan_create": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp,
                                         ctypes.POINTER(_vp)]),
+    "maxk_plan_create_rect": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32,
+                                             _vp, ctypes.POINTER(_vp)]),
     "maxk_plan_refresh_values": (ctypes.c_int, [_vp, _vp, _vp]),
     "maxk_plan_get_info": (ctypes.c_int, [_vp, _vp]),
     "maxk_plan_destroy": (ctypes.c_int, [_vp]),
@@ -54,6 +56,7 @@ class PlanInfo(ctypes.Structure):
         ("bwd_tasks", _i32),
         ("bwd_shared_blocks", _i32),
         ("device_bytes", _i64),
+        ("num_cols", _i32),
     ]
 
     def as_dict(self):

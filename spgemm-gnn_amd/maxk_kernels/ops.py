@@ -115,15 +115,45 @@ def maxk_backward(grad_output: torch.Tensor, indices: torch.Tensor,
 class GraphPlan:
     """Owns one ``maxk_plan`` (device partition metadata for a CSR graph, k and D)."""
 
-    def __init__(self, ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k):
+    def __init__(self, ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k,
+                 num_cols: Optional[int] = None):
         self.handle = ctypes.c_void_p(0)
         self.device = ptr.device
         self._refs = (ptr, idx, val)  # keep the graph's storage alive while cached
         self.val_version = val._version if val is not None else -1
+        self.num_rows = int(num_nodes)
+        self.num_cols = int(num_nodes if num_cols is None else num_cols)
+        self.num_edges = int(num_edges)
+        self.dim_origin = int(dim_origin)
+        self.dim_k = int(dim_k)
         with torch.cuda.device(ptr.device):
-            check(lib.maxk_plan_create(_p(ptr), _p(idx), _p(val), num_nodes, num_edges,
-                                       dim_origin, dim_k, _stream(),
-                                       ctypes.byref(self.handle)), "maxk_plan_create")
+            check(lib.maxk_plan_create_rect(_p(ptr), _p(idx), _p(val), self.num_rows,
+                                            self.num_cols, self.num_edges, self.dim_origin,
+                                            self.dim_k, _stream(), ctypes.byref(self.handle)),
+                  "maxk_plan_create")
+
+    def forward(self, sp_data, sp_index, out=None) -> torch.Tensor:
+        """SpGEMM with this plan: sp tables [num_cols, k] -> out [num_rows, D]."""
+        ptr, idx, val = self._refs
+        if out is None:
+            out = torch.empty((self.num_rows, self.dim_origin), dtype=torch.float32,
+                              device=sp_data.device)
+        check(lib.maxk_spgemm_forward(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
+                                      _p(sp_index), _p(out), self.num_rows, self.num_edges,
+                                      self.dim_k, self.dim_origin, _stream()), "spgemm_forward")
+        return out
+
+    def backward(self, grad_out, sp_index, grad_sp=None) -> torch.Tensor:
+        """SSpMM with this plan: grad_out [num_rows, D] -> grad_sp [num_cols, k]."""
+        ptr, idx, val = self._refs
+        if grad_sp is None:
+            grad_sp = torch.empty((self.num_cols, self.dim_k), dtype=torch.float32,
+                                  device=grad_out.device)
+        check(lib.maxk_sspmm_backward(self.handle, _p(ptr), _p(idx), _p(val), _p(grad_out),
+                                      _p(sp_index), _p(grad_sp), self.num_rows,
+                                      self.num_edges, self.dim_k, self.dim_origin, _stream()),
+              "spgemm_backward")
+        return grad_sp
 
     def refresh_values(self, val: torch.Tensor) -> None:
         with torch.cuda.device(self.device):
