@@ -11,7 +11,8 @@
 namespace maxk {
 
 constexpr int kWave = 64;               // CDNA wavefront width (never 32)
-constexpr int kFwdTileRows = 16;        // destination rows per forward work-group
+constexpr int kFwdTileRows = 16;        // default destination rows per forward work-group
+constexpr int kFwdMaxTileRows = 32;
 constexpr int kFwdThreads = 256;        // 4 waves
 constexpr int kBwdThreads = 512;        // 8 waves
 constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
@@ -58,6 +59,13 @@ struct FwdTask {
   int32_t e1;
 };
 static_assert(sizeof(FwdTask) == 16, "FwdTask is loaded as one dwordx4");
+
+// Packed CBSR record size for k (k % 4 == 0): k f32 values + k u8 selectors, rounded to
+// 64 B when that fits one 64-B sector, else to whole 128-B lines.
+inline int cbsr_record_bytes(int k) {
+  const int b = 5 * k;
+  return b <= 64 ? 64 : (b + 127) / 128 * 128;
+}
 
 // Backward work item: edges [e0, e1) of the column-block-major, row-sorted edge list, all
 // with source column in [col0, col0 + ncols). shared != 0: the block is split over several
@@ -110,11 +118,16 @@ struct maxk_plan {
   const int32_t* src_ptr = nullptr;  // identity of the graph the plan was built for
   const int32_t* src_idx = nullptr;
   // forward
+  int32_t fwd_tile_rows = 16;
+  int32_t fwd_acc = MAXK_ACC_F64;
+  int32_t fwd_rec_bytes = 0;     // packed CBSR record size (k % 4 == 0)
+  uint8_t* fwd_rec = nullptr;    // [num_cols][fwd_rec_bytes] workspace (per call pack)
   maxk::FwdTask* fwd_tasks = nullptr;
   int32_t n_fwd_tasks = 0;
   int32_t* zero_rows = nullptr;  // rows written by split tasks (atomic), zeroed first
   int32_t n_zero_rows = 0;
   // backward
+  int32_t bwd_acc = MAXK_ACC_F64;
   int32_t bwd_block_cols = 0;
   int32_t n_bwd_blocks = 0;
   maxk::BwdTask* bwd_tasks = nullptr;

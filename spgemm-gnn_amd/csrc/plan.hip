@@ -22,7 +22,7 @@
 
 namespace maxk {
 
-size_t bwd_lds_bytes(int block_cols, int k);
+size_t acc_bytes(int acc);
 
 
 __global__ void expand_rows_kernel(const int32_t* __restrict__ ptr, int N,
@@ -89,6 +89,7 @@ static int grid_for(int64_t n, int threads) {
 static void free_plan(maxk_plan* p) {
   if (!p) return;
   dfree(p->fwd_tasks);
+  dfree(p->fwd_rec);
   dfree(p->zero_rows);
   dfree(p->bwd_tasks);
   dfree(p->bwd_perm);
@@ -99,13 +100,12 @@ static void free_plan(maxk_plan* p) {
 }
 
 // Forward task list from a host copy of ptr.
-static void build_fwd_tasks(const std::vector<int32_t>& hp, int N, std::vector<FwdTask>& tasks,
-                            std::vector<int32_t>& zero_rows) {
-  const int R = kFwdTileRows;
+static void build_fwd_tasks(const std::vector<int32_t>& hp, int N, int R, int64_t cap_opt,
+                            std::vector<FwdTask>& tasks, std::vector<int32_t>& zero_rows) {
   const int64_t E = hp[N];
   const int ntiles = (N + R - 1) / R;
   const int64_t avg = ntiles ? (E + ntiles - 1) / ntiles : 0;
-  const int64_t cap = std::max<int64_t>(4096, 4 * avg);
+  const int64_t cap = cap_opt > 0 ? cap_opt : std::max<int64_t>(4096, 4 * avg);
   auto push_rows = [&](int r0, int r1) {
     if (r1 > r0) tasks.push_back(FwdTask{r0, r1 - r0, hp[r0], hp[r1]});
   };
@@ -149,7 +149,24 @@ extern "C" int maxk_plan_create(const int32_t* ptr, const int32_t* idx, const fl
 extern "C" int maxk_plan_create_rect(const int32_t* ptr, const int32_t* idx, const float* val,
                                      int32_t N, int32_t NC, int64_t E, int32_t D, int32_t k,
                                      void* stream, maxk_plan** out_plan) {
+  return maxk_plan_create_ex(ptr, idx, val, N, NC, E, D, k, nullptr, stream, out_plan);
+}
+
+extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const float* val,
+                                   int32_t N, int32_t NC, int64_t E, int32_t D, int32_t k,
+                                   const maxk_plan_options* opts, void* stream,
+                                   maxk_plan** out_plan) {
   MAXK_CHECK_ARG(out_plan != nullptr, "maxk_plan_create: out_plan is null");
+  maxk_plan_options o{};
+  if (opts) o = *opts;
+  MAXK_CHECK_ARG(o.fwd_tile_rows >= 0 && o.fwd_tile_rows <= kFwdMaxTileRows,
+                 "maxk_plan_create: fwd_tile_rows must be in [0, 32]");
+  MAXK_CHECK_ARG(o.fwd_accumulator >= 0 && o.fwd_accumulator <= MAXK_ACC_F32_CAS &&
+                     o.bwd_accumulator >= 0 && o.bwd_accumulator <= MAXK_ACC_F32_CAS,
+                 "maxk_plan_create: unknown accumulator kind");
+  MAXK_CHECK_ARG(o.bwd_lds_bytes >= 0 && o.bwd_lds_bytes <= 160 * 1024 &&
+                     o.bwd_tasks_per_cu >= 0 && o.fwd_task_cap >= 0,
+                 "maxk_plan_create: bad option value");
   *out_plan = nullptr;
   MAXK_CHECK_ARG(NC >= 0 && (E == 0 || NC > 0), "maxk_plan_create: num_cols out of range");
   MAXK_CHECK_ARG(N >= 0 && E >= 0 && E < (int64_t)INT32_MAX,
@@ -167,6 +184,9 @@ extern "C" int maxk_plan_create_rect(const int32_t* ptr, const int32_t* idx, con
   p->dim_k = k;
   p->src_ptr = ptr;
   p->src_idx = idx;
+  p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
+  p->fwd_acc = o.fwd_accumulator ? o.fwd_accumulator : MAXK_ACC_F64;
+  p->bwd_acc = o.bwd_accumulator ? o.bwd_accumulator : MAXK_ACC_F32_CAS;
 
   int32_t* row_of = nullptr;
   uint32_t* keys_in = nullptr;
@@ -211,7 +231,7 @@ extern "C" int maxk_plan_create_rect(const int32_t* ptr, const int32_t* idx, con
   }
   std::vector<FwdTask> ftasks;
   std::vector<int32_t> zrows;
-  build_fwd_tasks(hp, N, ftasks, zrows);
+  build_fwd_tasks(hp, N, p->fwd_tile_rows, o.fwd_task_cap, ftasks, zrows);
   p->n_fwd_tasks = (int32_t)ftasks.size();
   p->n_zero_rows = (int32_t)zrows.size();
   if (!ftasks.empty()) {
@@ -227,6 +247,12 @@ extern "C" int maxk_plan_create_rect(const int32_t* ptr, const int32_t* idx, con
     p->device_bytes += sizeof(int32_t) * zrows.size();
   }
 
+  if (k % 4 == 0 && NC > 0) {
+    p->fwd_rec_bytes = cbsr_record_bytes(k);
+    PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)NC * p->fwd_rec_bytes));
+    p->device_bytes += (int64_t)NC * p->fwd_rec_bytes;
+  }
+
   // ---------------- backward
   // Column blocks of C columns (k f64 accumulators each, <= kBwdLdsBudget of LDS: one
   // 512-thread work-group per CU); each block's edge range is cut into chunks so that about
@@ -240,7 +266,8 @@ extern "C" int maxk_plan_create_rect(const int32_t* ptr, const int32_t* idx, con
         cus = prop.multiProcessorCount;
     }
   }
-  int C = std::max(1, kBwdLdsBudget / (k * (int)sizeof(double)));
+  const int lds_budget = o.bwd_lds_bytes ? o.bwd_lds_bytes : kBwdLdsBudget;
+  int C = std::max(1, lds_budget / (k * (int)acc_bytes(p->bwd_acc)));
   C = std::min(C, std::max(NC, 1));
   const int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
   p->bwd_block_cols = C;
@@ -288,7 +315,7 @@ extern "C" int maxk_plan_create_rect(const int32_t* ptr, const int32_t* idx, con
     }
     for (int b = 0; b <= nblocks; ++b) offs[b] = offs32[b];
   }
-  const int64_t target_tasks = 2 * (int64_t)cus;
+  const int64_t target_tasks = (int64_t)(o.bwd_tasks_per_cu ? o.bwd_tasks_per_cu : 4) * cus;
   const int chunks = (int)std::max<int64_t>(1, (target_tasks + nblocks - 1) / std::max(nblocks, 1));
   std::vector<BwdTask> btasks;
   int nshared = 0;

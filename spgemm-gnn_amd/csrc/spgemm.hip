@@ -6,44 +6,94 @@
 // row (".warp4" metadata), accumulate into a per-warp LDS row and write it back with one
 // global float atomic per feature per chunk (forward), or scatter every product with a
 // global float atomic into grad_sp (backward). On MI355X global float atomics execute at
-// the memory side at ~1.3 TB/s, so both are restructured here:
+// the memory side (~1.3 TB/s of added bytes) and LDS ds_add_f32 runs at ~1/30 of the
+// integer LDS atomic rate (tools/ubench_atomics.hip, profiles/r01/ubench_atomics.log), so
+// both kernels are restructured:
 //
-//   forward : a 256-thread work-group owns <= 16 whole destination rows (LDS accumulator
-//             16 x D f32); its edges are processed flat (64/(k/4) edges per wave
-//             instruction, 4 features per lane: one dwordx4 value load + one dword
-//             selector load), scattered into LDS with ds_add_f32, and the rows are written
-//             back once with coalesced dwordx4 stores. Only rows longer than the task cap
-//             are split, and only those use global atomics.
+//   forward : a 256-thread work-group owns <= 32 whole destination rows (LDS accumulator
+//             rows x D); its edges are processed flat, k/4 lanes per edge, 4 features per
+//             lane (one dwordx4 value gather + one dword selector gather), U independent
+//             sub-steps in flight per wave; products are accumulated in LDS with f64
+//             atomics (ds_add_f64, ~9x the f32 rate) or an f32 compare-and-swap loop, and
+//             the rows are written back once with coalesced dwordx4 stores. Only rows
+//             longer than the task cap are split, and only those touch global atomics.
 //   backward: a 512-thread work-group owns a block of source columns whose k-wide
-//             gradients live in LDS; it sweeps the block's edges in destination-row
-//             order (plan-built block-major edge list), gathering grad_out[r, sel] and
-//             accumulating into LDS; the block is stored (or atomically flushed when a
-//             block is shared by several work-groups) once at the end.
+//             gradients live in LDS; it sweeps the block's edges in destination-row order
+//             (plan-built block-major edge list), so the lanes of one instruction gather
+//             from few rows of grad_out (L1 reuse); the block is stored (or atomically
+//             flushed when it is split over several work-groups) once at the end.
+#include <algorithm>
+
 #include "common.h"
 
 namespace maxk {
 
+// Accumulator kinds: MAXK_ACC_F64 (double, ds_add_f64) and MAXK_ACC_F32_CAS (float,
+// ds_read + ds_cmpst_rtn_b32 loop: the integer CAS path runs at the f64-atomic rate).
+template <int ACC>
+struct LdsAcc;
+
+template <>
+struct LdsAcc<MAXK_ACC_F64> {
+  using T = double;
+  static __device__ __forceinline__ void add(double* p, float v) { lds_add(p, (double)v); }
+};
+
+template <>
+struct LdsAcc<MAXK_ACC_F32_CAS> {
+  using T = float;
+  static __device__ __forceinline__ void add(float* p, float v) {
+    unsigned* u = reinterpret_cast<unsigned*>(p);
+    unsigned old = *u;
+    while (true) {
+      const unsigned assumed = old;
+      old = atomicCAS(u, assumed, __float_as_uint(__uint_as_float(assumed) + v));
+      if (old == assumed) break;
+    }
+  }
+};
+
 // --------------------------------------------------------------------------------------
 // forward
 // --------------------------------------------------------------------------------------
-template <int VEC>
+// CBSR records: the API hands over two tables (sp_data [N,k] f32, sp_index [N,k] u8), so an
+// edge's gather touches two cache lines. The forward first packs them into one record per
+// node, {k values, k selectors, pad} of rec_bytes (128 B at k = 16): one line per edge.
+// On gfx950 the gather is bound by L1/TA request count, not by bytes or by where the line
+// is served from (tools/ubench_gather.hip: 2.70 ms -> 1.84 ms for Reddit at k = 16).
+__global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
+                                 const uint8_t* __restrict__ sp_index,
+                                 uint8_t* __restrict__ rec, int ncols, int k, int rec_bytes) {
+  const int words = k + k / 4;  // k value words + k/4 selector words (k % 4 == 0)
+  const int64_t total = (int64_t)ncols * words;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = t / words;
+    const int w = (int)(t - c * words);
+    uint32_t v;
+    if (w < k) v = __float_as_uint(sp_data[c * k + w]);
+    else v = reinterpret_cast<const uint32_t*>(sp_index + c * k)[w - k];
+    reinterpret_cast<uint32_t*>(rec + c * rec_bytes)[w] = v;
+  }
+}
+
+template <int VEC, int ACC>
 __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     const FwdTask* __restrict__ tasks, const int32_t* __restrict__ ptr,
     const int32_t* __restrict__ idx, const float* __restrict__ val,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
-    float* __restrict__ out, int D, int k) {
-  // f64 LDS accumulators: on gfx950 ds_add_f64 sustains ~9x the rate of ds_add_f32
-  // (tools/ubench_atomics: 1.85e12 vs 2.0e11 adds/s chip-wide), and f64 sums make the
-  // f32 result independent of the atomic arrival order in all but pathological cases.
+    const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
+    int tile_rows) {
+  using A = LdsAcc<ACC>;
+  using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
   const FwdTask t = tasks[blockIdx.x];
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
-  double* acc = smem_d;
-  int* sptr = reinterpret_cast<int*>(smem_d + kFwdTileRows * D);
+  T* acc = reinterpret_cast<T*>(smem_d);
+  int* sptr = reinterpret_cast<int*>(acc + (size_t)tile_rows * D);
   const int n = nrows * D;
-  for (int i = threadIdx.x * 2; i < n; i += kFwdThreads * 2)
-    *reinterpret_cast<double2*>(acc + i) = make_double2(0.0, 0.0);
+  for (int i = threadIdx.x; i < n; i += kFwdThreads) acc[i] = T(0);
   for (int i = threadIdx.x; i <= nrows; i += kFwdThreads)
     sptr[i] = split ? (i == 0 ? t.e0 : t.e1) : ptr[t.row0 + i];
   __syncthreads();
@@ -51,7 +101,7 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   // lanes per edge: VEC==4 => k % 4 == 0 and k/4 <= 64; VEC==1 => min(k, 64) lanes that
   // loop over the row's k entries.
   const int L = (VEC == 4) ? k / 4 : (k < kWave ? k : kWave);
-  const int EPS = kWave / L;      // edges per wave instruction
+  const int EPS = kWave / L;  // edges per wave instruction
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int slot = lane / L;
@@ -88,19 +138,19 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
       uint32_t sel[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const size_t off = (size_t)c[u] * k + l0;
-        x[u] = *reinterpret_cast<const float4*>(sp_data + off);
-        sel[u] = *reinterpret_cast<const uint32_t*>(sp_index + off);
+        const uint8_t* rp = rec + (size_t)c[u] * rec_bytes;
+        x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
+        sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (ok[u]) {
-          double* arow = acc + rl[u] * D;
+          T* arow = acc + rl[u] * D;
           const uint32_t sv = sel[u];
-          lds_add(arow + (sv & 0xffu), (double)(v[u] * x[u].x));
-          lds_add(arow + ((sv >> 8) & 0xffu), (double)(v[u] * x[u].y));
-          lds_add(arow + ((sv >> 16) & 0xffu), (double)(v[u] * x[u].z));
-          lds_add(arow + (sv >> 24), (double)(v[u] * x[u].w));
+          A::add(arow + (sv & 0xffu), v[u] * x[u].x);
+          A::add(arow + ((sv >> 8) & 0xffu), v[u] * x[u].y);
+          A::add(arow + ((sv >> 16) & 0xffu), v[u] * x[u].z);
+          A::add(arow + (sv >> 24), v[u] * x[u].w);
         }
       }
     }
@@ -115,10 +165,9 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
         }
         const int c = idx[e];
         const float v = val[e];
-        double* arow = acc + lo * D;
+        T* arow = acc + lo * D;
         const size_t rb = (size_t)c * k;
-        for (int l = l0; l < k; l += L)
-          lds_add(arow + sp_index[rb + l], (double)(v * sp_data[rb + l]));
+        for (int l = l0; l < k; l += L) A::add(arow + sp_index[rb + l], v * sp_data[rb + l]);
       }
     }
   }
@@ -127,12 +176,9 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   float* dst = out + (size_t)t.row0 * D;
   if (!split) {
     if ((D & 3) == 0) {
-      for (int i = threadIdx.x * 4; i < n; i += kFwdThreads * 4) {
-        const double2 a = *reinterpret_cast<const double2*>(acc + i);
-        const double2 b = *reinterpret_cast<const double2*>(acc + i + 2);
+      for (int i = threadIdx.x * 4; i < n; i += kFwdThreads * 4)
         *reinterpret_cast<float4*>(dst + i) =
-            make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
-      }
+            make_float4((float)acc[i], (float)acc[i + 1], (float)acc[i + 2], (float)acc[i + 3]);
     } else {
       for (int i = threadIdx.x; i < n; i += kFwdThreads) dst[i] = (float)acc[i];
     }
@@ -153,19 +199,22 @@ __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, fl
 // backward
 // --------------------------------------------------------------------------------------
 // Flat edge processing in (column block, destination row) order: the edges one wave
-// instruction covers share few rows of grad_out, so its gathers stay in the CU's L1.
-// Accumulation: f64 LDS atomics (ds_add_f64 ~9x the ds_add_f32 rate on gfx950; any wave
-// may update any column of the block, which is what keeps the row locality).
-template <int F>
+// instruction covers share few rows of grad_out, so its gathers stay in the CU's L1. Any
+// wave may update any column of the block (that is what keeps the row locality), hence the
+// atomic LDS accumulation.
+template <int F, int ACC>
 __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
     const BwdTask* __restrict__ tasks, const int32_t* __restrict__ erow,
     const int32_t* __restrict__ ecol, const float* __restrict__ evals,
     const float* __restrict__ G, const uint8_t* __restrict__ sp_index,
     float* __restrict__ grad_sp, int D, int k) {
-  extern __shared__ __align__(16) double bacc[];  // [ncols][k]
+  using A = LdsAcc<ACC>;
+  using T = typename A::T;
+  extern __shared__ __align__(16) double bsmem[];
+  T* bacc = reinterpret_cast<T*>(bsmem);  // [ncols][k]
   const BwdTask t = tasks[blockIdx.x];
   const int n = t.ncols * k;
-  for (int i = threadIdx.x; i < n; i += kBwdThreads) bacc[i] = 0.0;
+  for (int i = threadIdx.x; i < n; i += kBwdThreads) bacc[i] = T(0);
   __syncthreads();
 
   const int L = bwd_lanes(k);
@@ -209,11 +258,11 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (ok[u]) {
-          double* a = bacc + (c[u] - t.col0) * k + q * 4;
-          lds_add(a, (double)(v[u] * g[u][0]));
-          lds_add(a + 1, (double)(v[u] * g[u][1]));
-          lds_add(a + 2, (double)(v[u] * g[u][2]));
-          lds_add(a + 3, (double)(v[u] * g[u][3]));
+          T* a = bacc + (c[u] - t.col0) * k + q * 4;
+          A::add(a, v[u] * g[u][0]);
+          A::add(a + 1, v[u] * g[u][1]);
+          A::add(a + 2, v[u] * g[u][2]);
+          A::add(a + 3, v[u] * g[u][3]);
         }
       }
     } else {
@@ -222,8 +271,8 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
         if (ok[u]) {
           const float* grow = G + (size_t)r[u] * D;
           const uint8_t* srow = sp_index + (size_t)c[u] * k;
-          double* a = bacc + (c[u] - t.col0) * k;
-          for (int l = q; l < k; l += L) lds_add(a + l, (double)(v[u] * grow[srow[l]]));
+          T* a = bacc + (c[u] - t.col0) * k;
+          for (int l = q; l < k; l += L) A::add(a + l, v[u] * grow[srow[l]]);
         }
       }
     }
@@ -263,11 +312,21 @@ __global__ __launch_bounds__(256) void dense_spmm_kernel(
   }
 }
 
-static size_t fwd_lds_bytes(int D) {
-  return (size_t)kFwdTileRows * D * sizeof(double) + (kFwdTileRows + 1) * sizeof(int);
+size_t acc_bytes(int acc) { return acc == MAXK_ACC_F32_CAS ? sizeof(float) : sizeof(double); }
+
+size_t fwd_lds_bytes(int tile_rows, int D, int acc) {
+  return (size_t)tile_rows * D * acc_bytes(acc) + (tile_rows + 1) * sizeof(int);
 }
 
-size_t bwd_lds_bytes(int block_cols, int k) { return (size_t)block_cols * k * sizeof(double); }
+size_t bwd_lds_bytes(int block_cols, int k, int acc) {
+  return (size_t)block_cols * k * acc_bytes(acc);
+}
+
+template <typename K>
+static hipError_t allow_lds(K* kernel, size_t bytes) {
+  return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes);
+}
 
 }  // namespace maxk
 
@@ -302,13 +361,31 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
                        plan->zero_rows, plan->n_zero_rows, out, D);
     MAXK_LAUNCH_CHECK("zero_rows launch");
   }
-  const size_t lds = fwd_lds_bytes(D);
-  if (k % 4 == 0)
-    hipLaunchKernelGGL(spgemm_fwd_kernel<4>, dim3(plan->n_fwd_tasks), dim3(kFwdThreads), lds,
-                       s, plan->fwd_tasks, ptr, idx, val, sp_data, sp_index, out, D, k);
-  else
-    hipLaunchKernelGGL(spgemm_fwd_kernel<1>, dim3(plan->n_fwd_tasks), dim3(kFwdThreads), lds,
-                       s, plan->fwd_tasks, ptr, idx, val, sp_data, sp_index, out, D, k);
+  const int R = plan->fwd_tile_rows;
+  const size_t lds = fwd_lds_bytes(R, D, plan->fwd_acc);
+  const int rec_bytes = plan->fwd_rec_bytes;
+  if (k % 4 == 0 && plan->num_cols > 0) {
+    const int64_t words = (int64_t)plan->num_cols * (k + k / 4);
+    const int grid = (int)std::min<int64_t>((words + 255) / 256, 65536);
+    hipLaunchKernelGGL(pack_cbsr_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
+                       plan->fwd_rec, plan->num_cols, k, rec_bytes);
+    MAXK_LAUNCH_CHECK("pack_cbsr launch");
+  }
+  const dim3 grid(plan->n_fwd_tasks), block(kFwdThreads);
+#define FWD_LAUNCH(V, A)                                                                  \
+  do {                                                                                    \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, A>, lds));          \
+    hipLaunchKernelGGL((spgemm_fwd_kernel<V, A>), grid, block, lds, s, plan->fwd_tasks, ptr, \
+                       idx, val, sp_data, sp_index, plan->fwd_rec, rec_bytes, out, D, k, R); \
+  } while (0)
+  if (k % 4 == 0) {
+    if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(4, MAXK_ACC_F32_CAS);
+    else FWD_LAUNCH(4, MAXK_ACC_F64);
+  } else {
+    if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(1, MAXK_ACC_F32_CAS);
+    else FWD_LAUNCH(1, MAXK_ACC_F64);
+  }
+#undef FWD_LAUNCH
   MAXK_LAUNCH_CHECK("spgemm_fwd launch");
   return MAXK_OK;
 }
@@ -329,24 +406,24 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   hipStream_t s = (hipStream_t)stream;
   if (plan->n_bwd_shared > 0)
     MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)plan->num_cols * k * sizeof(float), s));
-  const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k);
   if (plan->n_bwd_tasks == 0) return MAXK_OK;
-  static bool attr_set = false;  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB/CU)
-  if (!attr_set) {
-    MAXK_HIP_TRY(hipFuncSetAttribute((const void*)sspmm_bwd_kernel<4>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLdsBudget));
-    MAXK_HIP_TRY(hipFuncSetAttribute((const void*)sspmm_bwd_kernel<1>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLdsBudget));
-    attr_set = true;
+  const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k, plan->bwd_acc);
+  const dim3 grid(plan->n_bwd_tasks), block(kBwdThreads);
+#define BWD_LAUNCH(F, A)                                                                  \
+  do {                                                                                    \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd_kernel<F, A>, lds));           \
+    hipLaunchKernelGGL((sspmm_bwd_kernel<F, A>), grid, block, lds, s, plan->bwd_tasks,    \
+                       plan->bwd_row, plan->bwd_col, plan->bwd_val, grad_out, sp_index,   \
+                       grad_sp, D, k);                                                    \
+  } while (0)
+  if (bwd_feats(k) == 4) {
+    if (plan->bwd_acc == MAXK_ACC_F32_CAS) BWD_LAUNCH(4, MAXK_ACC_F32_CAS);
+    else BWD_LAUNCH(4, MAXK_ACC_F64);
+  } else {
+    if (plan->bwd_acc == MAXK_ACC_F32_CAS) BWD_LAUNCH(1, MAXK_ACC_F32_CAS);
+    else BWD_LAUNCH(1, MAXK_ACC_F64);
   }
-  if (bwd_feats(k) == 4)
-    hipLaunchKernelGGL(sspmm_bwd_kernel<4>, dim3(plan->n_bwd_tasks), dim3(kBwdThreads), lds, s,
-                       plan->bwd_tasks, plan->bwd_row, plan->bwd_col, plan->bwd_val, grad_out,
-                       sp_index, grad_sp, D, k);
-  else
-    hipLaunchKernelGGL(sspmm_bwd_kernel<1>, dim3(plan->n_bwd_tasks), dim3(kBwdThreads), lds, s,
-                       plan->bwd_tasks, plan->bwd_row, plan->bwd_col, plan->bwd_val, grad_out,
-                       sp_index, grad_sp, D, k);
+#undef BWD_LAUNCH
   MAXK_LAUNCH_CHECK("sspmm_bwd launch");
   return MAXK_OK;
 }

@@ -29,6 +29,8 @@ SIGNATURES = {
                                         ctypes.POINTER(_vp)]),
     "maxk_plan_create_rect": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32,
                                              _vp, ctypes.POINTER(_vp)]),
+    "maxk_plan_create_ex": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _vp,
+                                           _vp, ctypes.POINTER(_vp)]),
     "maxk_plan_refresh_values": (ctypes.c_int, [_vp, _vp, _vp]),
     "maxk_plan_get_info": (ctypes.c_int, [_vp, _vp]),
     "maxk_plan_destroy": (ctypes.c_int, [_vp]),
@@ -39,6 +41,23 @@ SIGNATURES = {
     "maxk_dense_spmm_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),
     "maxk_warp4_build": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
 }
+
+
+class PlanOptions(ctypes.Structure):
+    """Mirror of ``maxk_plan_options`` (0 = default for every field)."""
+
+    _fields_ = [
+        ("fwd_tile_rows", _i32),
+        ("fwd_accumulator", _i32),
+        ("bwd_lds_bytes", _i32),
+        ("bwd_accumulator", _i32),
+        ("bwd_tasks_per_cu", _i32),
+        ("fwd_task_cap", _i32),
+        ("reserved", _i32 * 2),
+    ]
+
+
+ACC_KINDS = {"auto": 0, "f64": 1, "f32_cas": 2}
 
 
 class PlanInfo(ctypes.Structure):

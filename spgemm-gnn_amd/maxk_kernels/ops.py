@@ -23,7 +23,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import PlanInfo, check, lib
+from ._lib import ACC_KINDS, PlanInfo, PlanOptions, check, lib
 
 TOPK_MODES = {"exact": 0, "ref_compat": 1}
 
@@ -116,7 +116,7 @@ class GraphPlan:
     """Owns one ``maxk_plan`` (device partition metadata for a CSR graph, k and D)."""
 
     def __init__(self, ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k,
-                 num_cols: Optional[int] = None):
+                 num_cols: Optional[int] = None, options: Optional[dict] = None):
         self.handle = ctypes.c_void_p(0)
         self.device = ptr.device
         self._refs = (ptr, idx, val)  # keep the graph's storage alive while cached
@@ -126,11 +126,16 @@ class GraphPlan:
         self.num_edges = int(num_edges)
         self.dim_origin = int(dim_origin)
         self.dim_k = int(dim_k)
+        opts = PlanOptions()
+        for key, value in (options or {}).items():
+            if key in ("fwd_accumulator", "bwd_accumulator") and isinstance(value, str):
+                value = ACC_KINDS[value]
+            setattr(opts, key, int(value))
         with torch.cuda.device(ptr.device):
-            check(lib.maxk_plan_create_rect(_p(ptr), _p(idx), _p(val), self.num_rows,
-                                            self.num_cols, self.num_edges, self.dim_origin,
-                                            self.dim_k, _stream(), ctypes.byref(self.handle)),
-                  "maxk_plan_create")
+            check(lib.maxk_plan_create_ex(_p(ptr), _p(idx), _p(val), self.num_rows,
+                                          self.num_cols, self.num_edges, self.dim_origin,
+                                          self.dim_k, ctypes.byref(opts), _stream(),
+                                          ctypes.byref(self.handle)), "maxk_plan_create")
 
     def forward(self, sp_data, sp_index, out=None) -> torch.Tensor:
         """SpGEMM with this plan: sp tables [num_cols, k] -> out [num_rows, D]."""

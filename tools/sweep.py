@@ -1,0 +1,90 @@
+"""Plan-option sweep on the BASELINE workload (tooling; run on the GPU box).
+
+  python tools/sweep.py [--k 16] [--dataset reddit]
+
+Times the SpGEMM forward and SSpMM backward for several maxk_plan_options in one process
+(HIP events, median of 5 x 10 launches), and checks each variant's output against the
+first (default) variant.
+"""
+import argparse
+import itertools
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "spgemm-gnn_amd"))
+
+import torch  # noqa: E402
+
+import maxk_kernels as mk  # noqa: E402
+from maxk_kernels import graphs  # noqa: E402
+
+
+def timeit(fn, reps=10, rounds=5):
+    ts = []
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e) / reps)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=16)
+    ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--dataset", default="reddit")
+    ap.add_argument("--which", default="both", choices=["fwd", "bwd", "both"])
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    n, e = graphs.DATASETS[args.dataset]
+    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    val = graphs.sage_mean_values(ptr)
+    e = idx.numel()
+    h = graphs.features(n, args.dim, seed=97, device=dev)
+    g = graphs.features(n, args.dim, seed=98, device=dev)
+    sp_data, sp_index = mk.maxk_forward(h, args.k, return_index=True)
+    del h
+
+    fwd_variants = [dict()] + [dict(fwd_tile_rows=r, fwd_accumulator=a)
+                               for r, a in itertools.product((8, 16, 32), ("f64", "f32_cas"))]
+    bwd_variants = [dict()] + [dict(bwd_lds_bytes=b, bwd_accumulator=a, bwd_tasks_per_cu=t)
+                               for b, a, t in itertools.product((76800, 153600), ("f64", "f32_cas"),
+                                                                (1, 2, 4))]
+    ref_out = ref_grad = None
+    results = []
+    if args.which in ("fwd", "both"):
+        for opt in fwd_variants:
+            plan = mk.GraphPlan(ptr, idx, val, n, e, args.dim, args.k, options=opt)
+            out = plan.forward(sp_data, sp_index)
+            ms = timeit(lambda: plan.forward(sp_data, sp_index, out))
+            if ref_out is None:
+                ref_out = out.clone()
+            err = float(((out - ref_out).abs() / (ref_out.abs() + 1e-3)).max())
+            results.append({"kernel": "fwd", "opts": opt, "ms": ms, "gedges_s": e / ms / 1e6,
+                            "max_rel_dev": err, "info": plan.info()})
+            print(json.dumps(results[-1]), flush=True)
+            del plan
+    if args.which in ("bwd", "both"):
+        for opt in bwd_variants:
+            plan = mk.GraphPlan(ptr, idx, val, n, e, args.dim, args.k, options=opt)
+            grad = plan.backward(g, sp_index)
+            ms = timeit(lambda: plan.backward(g, sp_index, grad))
+            if ref_grad is None:
+                ref_grad = grad.clone()
+            err = float(((grad - ref_grad).abs() / (ref_grad.abs() + 1e-3)).max())
+            results.append({"kernel": "bwd", "opts": opt, "ms": ms, "gedges_s": e / ms / 1e6,
+                            "max_rel_dev": err, "info": plan.info()})
+            print(json.dumps(results[-1]), flush=True)
+            del plan
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
