@@ -11,7 +11,7 @@
 namespace maxk {
 
 constexpr int kWave = 64;               // CDNA wavefront width (never 32)
-constexpr int kFwdTileRows = 16;        // default destination rows per forward work-group
+constexpr int kFwdTileRows = 32;        // default destination rows per forward work-group
 constexpr int kFwdMaxTileRows = 32;
 constexpr int kFwdThreads = 256;        // 4 waves
 constexpr int kBwdThreads = 512;        // 8 waves
@@ -49,9 +49,10 @@ void set_error(const std::string& msg);
     }                                                                           \
   } while (0)
 
-// Forward work item: a run of whole destination rows [row0, row0+nrows) with edge range
-// [e0, e1) = [ptr[row0], ptr[row0+nrows]), or (split=1) one segment of a long row whose
-// partial sum is added atomically into a row pre-zeroed by zero_rows.
+// Forward work item: a run of whole destination rows [row0, row0+nrows) (or, nrows < 0, one
+// segment of a long row whose partial sum is added atomically into a row pre-zeroed by
+// zero_rows), with edge range [e0, e1) of the plan's permuted edge order (the task's CSR
+// edges sorted by column).
 struct FwdTask {
   int32_t row0;
   int32_t nrows;
@@ -122,7 +123,10 @@ struct maxk_plan {
   int32_t fwd_acc = MAXK_ACC_F64;
   int32_t fwd_rec_bytes = 0;     // packed CBSR record size (k % 4 == 0)
   uint8_t* fwd_rec = nullptr;    // [num_cols][fwd_rec_bytes] workspace (per call pack)
-  maxk::FwdTask* fwd_tasks = nullptr;
+  maxk::FwdTask* fwd_tasks = nullptr;   // e0/e1 index the permuted edge order below
+  int32_t* fwd_perm = nullptr;   // CSR edge id of each permuted forward edge
+  uint32_t* fwd_cr = nullptr;    // column | (row within the task << 27)
+  float* fwd_val = nullptr;      // val snapshot in the permuted order
   int32_t n_fwd_tasks = 0;
   int32_t* zero_rows = nullptr;  // rows written by split tasks (atomic), zeroed first
   int32_t n_zero_rows = 0;

@@ -34,6 +34,42 @@ __global__ void expand_rows_kernel(const int32_t* __restrict__ ptr, int N,
   for (int e = ptr[row] + lane; e < e1; e += kWave) row_of[e] = row;
 }
 
+// Forward edge order: every forward task's edges contiguous (tasks in launch order) and
+// sorted by source column inside the task, so the work-groups running at the same time -
+// similar-sized tasks, heavy first - sweep the CBSR table in step and its recently used
+// records stay in L2. starts/ranks/row0s: the tasks sorted by their first CSR edge.
+__global__ void fwd_key_kernel(const int32_t* __restrict__ idx, const int32_t* __restrict__ row_of,
+                               int64_t E, const int32_t* __restrict__ starts,
+                               const int32_t* __restrict__ ranks,
+                               const int32_t* __restrict__ row0s, int ntasks, int cbits,
+                               uint64_t* __restrict__ keys, int32_t* __restrict__ ids,
+                               int32_t* __restrict__ rl_of) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = ntasks - 1;  // last task whose first edge <= e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (starts[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    keys[e] = ((uint64_t)ranks[lo] << cbits) | (uint64_t)(uint32_t)idx[e];
+    ids[e] = (int32_t)e;
+    rl_of[e] = row_of[e] - row0s[lo];
+  }
+}
+
+__global__ void gather_fwd_kernel(const int32_t* __restrict__ perm,
+                                  const int32_t* __restrict__ idx,
+                                  const int32_t* __restrict__ rl_of,
+                                  const float* __restrict__ val, int64_t E,
+                                  uint32_t* __restrict__ cr, float* __restrict__ fval) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < E;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t e = perm[j];
+    if (cr) cr[j] = (uint32_t)idx[e] | ((uint32_t)rl_of[e] << 27);
+    fval[j] = val ? val[e] : 1.0f;
+  }
+}
+
 // Sort key of each edge for the backward: its source-column block c / C (a stable radix
 // sort then yields the block-major, destination-row-sorted edge list). Also validates the
 // column ids: any idx outside [0, NC) sets *bad (the compute kernels index the CBSR tables
@@ -90,6 +126,9 @@ static void free_plan(maxk_plan* p) {
   if (!p) return;
   dfree(p->fwd_tasks);
   dfree(p->fwd_rec);
+  dfree(p->fwd_perm);
+  dfree(p->fwd_cr);
+  dfree(p->fwd_val);
   dfree(p->zero_rows);
   dfree(p->bwd_tasks);
   dfree(p->bwd_perm);
@@ -235,6 +274,78 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   p->n_fwd_tasks = (int32_t)ftasks.size();
   p->n_zero_rows = (int32_t)zrows.size();
   if (!ftasks.empty()) {
+    // permuted edge order (see fwd_key_kernel): tasks keep their CSR edge sets
+    const int nt = (int)ftasks.size();
+    std::vector<int32_t> order(nt);
+    for (int i = 0; i < nt; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(),
+              [&](int a, int b) { return ftasks[a].e0 < ftasks[b].e0; });
+    std::vector<int32_t> starts(nt), ranks(nt), row0s(nt);
+    for (int i = 0; i < nt; ++i) {
+      starts[i] = ftasks[order[i]].e0;
+      ranks[i] = order[i];
+      row0s[i] = ftasks[order[i]].row0;
+    }
+    int32_t pos = 0;
+    for (int i = 0; i < nt; ++i) {  // new contiguous ranges, launch order
+      const int32_t len = ftasks[i].e1 - ftasks[i].e0;
+      ftasks[i].e0 = pos;
+      ftasks[i].e1 = pos + len;
+      pos += len;
+    }
+    if (E > 0) {
+      int cbits = 1;
+      while ((1ll << cbits) < (long long)NC) ++cbits;
+      int tbits = 1;
+      while ((1ll << tbits) < (long long)nt) ++tbits;
+      int32_t *d_starts = nullptr, *d_ranks = nullptr, *d_row0s = nullptr, *d_rl = nullptr,
+              *d_ids = nullptr;
+      uint64_t *d_kin = nullptr, *d_kout = nullptr;
+      void* d_tmp = nullptr;
+      auto fwd_cleanup = [&]() {
+        dfree(d_starts); dfree(d_ranks); dfree(d_row0s); dfree(d_rl); dfree(d_ids);
+        dfree(d_kin); dfree(d_kout); dfree(d_tmp);
+      };
+#define FWD_TRY(expr)                         \
+  do {                                        \
+    hipError_t _e2 = (expr);                  \
+    if (_e2 != hipSuccess) {                  \
+      fwd_cleanup();                          \
+      PLAN_TRY(_e2);                          \
+    }                                         \
+  } while (0)
+      FWD_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
+      hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
+      FWD_TRY(hipMalloc(&d_starts, sizeof(int32_t) * nt));
+      FWD_TRY(hipMalloc(&d_ranks, sizeof(int32_t) * nt));
+      FWD_TRY(hipMalloc(&d_row0s, sizeof(int32_t) * nt));
+      FWD_TRY(hipMemcpyAsync(d_starts, starts.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s));
+      FWD_TRY(hipMemcpyAsync(d_ranks, ranks.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s));
+      FWD_TRY(hipMemcpyAsync(d_row0s, row0s.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s));
+      FWD_TRY(hipMalloc(&d_rl, sizeof(int32_t) * E));
+      FWD_TRY(hipMalloc(&d_ids, sizeof(int32_t) * E));
+      FWD_TRY(hipMalloc(&d_kin, sizeof(uint64_t) * E));
+      FWD_TRY(hipMalloc(&d_kout, sizeof(uint64_t) * E));
+      FWD_TRY(hipMalloc(&p->fwd_perm, sizeof(int32_t) * E));
+      hipLaunchKernelGGL(fwd_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, row_of, E,
+                         d_starts, d_ranks, d_row0s, nt, cbits, d_kin, d_ids, d_rl);
+      FWD_TRY(hipGetLastError());
+      size_t tb = 0;
+      FWD_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_kin, d_kout, d_ids, p->fwd_perm,
+                                                 (int)E, 0, cbits + tbits, s));
+      FWD_TRY(hipMalloc(&d_tmp, tb));
+      FWD_TRY(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_kin, d_kout, d_ids, p->fwd_perm,
+                                                 (int)E, 0, cbits + tbits, s));
+      FWD_TRY(hipMalloc(&p->fwd_cr, sizeof(uint32_t) * E));
+      FWD_TRY(hipMalloc(&p->fwd_val, sizeof(float) * E));
+      hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->fwd_perm,
+                         idx, d_rl, val, E, p->fwd_cr, p->fwd_val);
+      FWD_TRY(hipGetLastError());
+      FWD_TRY(hipStreamSynchronize(s));
+      fwd_cleanup();
+#undef FWD_TRY
+      p->device_bytes += (int64_t)E * 12;
+    }
     PLAN_TRY(hipMalloc(&p->fwd_tasks, sizeof(FwdTask) * ftasks.size()));
     PLAN_TRY(hipMemcpyAsync(p->fwd_tasks, ftasks.data(), sizeof(FwdTask) * ftasks.size(),
                             hipMemcpyHostToDevice, s));
@@ -274,14 +385,16 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   p->n_bwd_blocks = nblocks;
   std::vector<int64_t> offs(nblocks + 1, 0);
   if (E > 0) {
-    PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
+    if (!row_of) {
+      PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
+      hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
+    }
     PLAN_TRY(hipMalloc(&keys_in, sizeof(uint32_t) * E));
     PLAN_TRY(hipMalloc(&keys_out, sizeof(uint32_t) * E));
     PLAN_TRY(hipMalloc(&ids_in, sizeof(int32_t) * E));
     PLAN_TRY(hipMalloc(&p->bwd_perm, sizeof(int32_t) * E));
     PLAN_TRY(hipMalloc(&d_bad, sizeof(int)));
     PLAN_TRY(hipMemsetAsync(d_bad, 0, sizeof(int), s));
-    hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
     hipLaunchKernelGGL(bwd_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, E, C, NC,
                        keys_in, ids_in, d_bad);
     PLAN_TRY(hipGetLastError());
@@ -364,6 +477,10 @@ extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* st
   hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
                      (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
                      nullptr, nullptr, p->bwd_val);
+  if (p->fwd_perm)
+    hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
+                       (hipStream_t)stream, p->fwd_perm, nullptr, nullptr, val, p->num_edges,
+                       nullptr, p->fwd_val);
   MAXK_LAUNCH_CHECK("maxk_plan_refresh_values launch");
   return MAXK_OK;
 }

@@ -79,11 +79,10 @@ __global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
 
 template <int VEC, int ACC>
 __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
-    const FwdTask* __restrict__ tasks, const int32_t* __restrict__ ptr,
-    const int32_t* __restrict__ idx, const float* __restrict__ val,
-    const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
-    const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
-    int tile_rows) {
+    const FwdTask* __restrict__ tasks, const uint32_t* __restrict__ cr,
+    const float* __restrict__ fval, const float* __restrict__ sp_data,
+    const uint8_t* __restrict__ sp_index, const uint8_t* __restrict__ rec, int rec_bytes,
+    float* __restrict__ out, int D, int k, int tile_rows) {
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
@@ -91,11 +90,8 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
   T* acc = reinterpret_cast<T*>(smem_d);
-  int* sptr = reinterpret_cast<int*>(acc + (size_t)tile_rows * D);
   const int n = nrows * D;
   for (int i = threadIdx.x; i < n; i += kFwdThreads) acc[i] = T(0);
-  for (int i = threadIdx.x; i <= nrows; i += kFwdThreads)
-    sptr[i] = split ? (i == 0 ? t.e0 : t.e1) : ptr[t.row0 + i];
   __syncthreads();
 
   // lanes per edge: VEC==4 => k % 4 == 0 and k/4 <= 64; VEC==1 => min(k, 64) lanes that
@@ -108,16 +104,17 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   const int l0 = (lane - slot * L) * VEC;
   const bool lane_on = slot < EPS;
   constexpr int kWaves = kFwdThreads / kWave;
+  constexpr uint32_t kColMask = (1u << 27) - 1;
 
   if constexpr (VEC == 4) {
     // U sub-steps per iteration with every load issued before the first LDS update: the
-    // chain idx/val -> CBSR row -> LDS has two dependent global round trips, so memory-
-    // level parallelism comes from U independent sub-steps per wave. Out-of-range lanes
-    // load a clamped (valid) edge and skip the update.
+    // chain (col, val) -> CBSR record -> LDS has two dependent global round trips, so
+    // memory-level parallelism comes from U independent sub-steps per wave. Out-of-range
+    // lanes load a clamped (valid) edge and skip the update.
     constexpr int U = kFwdUnroll;
     const int last = t.e1 - 1;
     for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
-      int c[U], rl[U];
+      uint32_t cw[U];
       float v[U];
       bool ok[U];
 #pragma unroll
@@ -125,27 +122,21 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
         const int e = base + u * EPS + slot;
         ok[u] = lane_on && e < t.e1;
         const int ec = ok[u] ? e : last;
-        c[u] = idx[ec];
-        v[u] = val[ec];
-        int lo = 0, hi = nrows - 1;  // row of ec: last j with sptr[j] <= ec
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (sptr[mid] <= ec) lo = mid; else hi = mid - 1;
-        }
-        rl[u] = lo;
+        cw[u] = cr[ec];
+        v[u] = fval[ec];
       }
       float4 x[U];
       uint32_t sel[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint8_t* rp = rec + (size_t)c[u] * rec_bytes;
+        const uint8_t* rp = rec + (size_t)(cw[u] & kColMask) * rec_bytes;
         x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
         sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (ok[u]) {
-          T* arow = acc + rl[u] * D;
+          T* arow = acc + (cw[u] >> 27) * D;
           const uint32_t sv = sel[u];
           A::add(arow + (sv & 0xffu), v[u] * x[u].x);
           A::add(arow + ((sv >> 8) & 0xffu), v[u] * x[u].y);
@@ -158,15 +149,10 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
       const int e = base + slot;
       if (lane_on && e < t.e1) {
-        int lo = 0, hi = nrows - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (sptr[mid] <= e) lo = mid; else hi = mid - 1;
-        }
-        const int c = idx[e];
-        const float v = val[e];
-        T* arow = acc + lo * D;
-        const size_t rb = (size_t)c * k;
+        const uint32_t cwv = cr[e];
+        const float v = fval[e];
+        T* arow = acc + (cwv >> 27) * D;
+        const size_t rb = (size_t)(cwv & kColMask) * k;
         for (int l = l0; l < k; l += L) A::add(arow + sp_index[rb + l], v * sp_data[rb + l]);
       }
     }
@@ -315,7 +301,7 @@ __global__ __launch_bounds__(256) void dense_spmm_kernel(
 size_t acc_bytes(int acc) { return acc == MAXK_ACC_F32_CAS ? sizeof(float) : sizeof(double); }
 
 size_t fwd_lds_bytes(int tile_rows, int D, int acc) {
-  return (size_t)tile_rows * D * acc_bytes(acc) + (tile_rows + 1) * sizeof(int);
+  return (size_t)tile_rows * D * acc_bytes(acc);
 }
 
 size_t bwd_lds_bytes(int block_cols, int k, int acc) {
@@ -355,6 +341,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
   if (N == 0) return MAXK_OK;
   MAXK_CHECK_ARG(out && sp_data && sp_index && (E == 0 || (idx && val)) && ptr,
                  "maxk_spgemm_forward: null pointer");
+  (void)val;  // the plan holds the permuted snapshot of (idx, val)
   hipStream_t s = (hipStream_t)stream;
   if (plan->n_zero_rows > 0) {
     hipLaunchKernelGGL(zero_rows_kernel, dim3(plan->n_zero_rows), dim3(256), 0, s,
@@ -375,8 +362,9 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \
     if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, A>, lds));          \
-    hipLaunchKernelGGL((spgemm_fwd_kernel<V, A>), grid, block, lds, s, plan->fwd_tasks, ptr, \
-                       idx, val, sp_data, sp_index, plan->fwd_rec, rec_bytes, out, D, k, R); \
+    hipLaunchKernelGGL((spgemm_fwd_kernel<V, A>), grid, block, lds, s, plan->fwd_tasks,      \
+                       plan->fwd_cr, plan->fwd_val, sp_data, sp_index, plan->fwd_rec,      \
+                       rec_bytes, out, D, k, R);                                           \
   } while (0)
   if (k % 4 == 0) {
     if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(4, MAXK_ACC_F32_CAS);

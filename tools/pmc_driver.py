@@ -1,0 +1,31 @@
+"""Small fixed workload for rocprofv3 --pmc passes (tooling): the BASELINE config (Reddit,
+D=256, k=16), 3 SpGEMM forwards + 3 SSpMM backwards with the default plan."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "spgemm-gnn_amd"))
+import torch  # noqa: E402
+
+import maxk_kernels as mk  # noqa: E402
+from maxk_kernels import graphs  # noqa: E402
+
+k = int(os.environ.get("PMC_K", "16"))
+ds = os.environ.get("PMC_DATASET", "reddit")
+dev = torch.device("cuda:0")
+n, e = graphs.DATASETS[ds]
+ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+val = graphs.sage_mean_values(ptr)
+e = idx.numel()
+h = graphs.features(n, 256, seed=97, device=dev)
+g = graphs.features(n, 256, seed=98, device=dev)
+sp_data, sp_index = mk.maxk_forward(h, k, return_index=True)
+plan = mk.get_plan(ptr, idx, val, n, e, 256, k)
+out = plan.forward(sp_data, sp_index)
+grad = plan.backward(g, sp_index)
+for _ in range(3):
+    plan.forward(sp_data, sp_index, out)
+for _ in range(3):
+    plan.backward(g, sp_index, grad)
+torch.cuda.synchronize()
+print("done", plan.info())
