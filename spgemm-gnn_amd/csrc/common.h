@@ -82,15 +82,6 @@ struct BwdTask {
 };
 static_assert(sizeof(BwdTask) == 32, "BwdTask is 2 x dwordx4");
 
-__host__ __device__ inline int bwd_feats(int k) { return (k % 4 == 0) ? 4 : 1; }
-__host__ __device__ inline int bwd_lanes(int k) {
-  return bwd_feats(k) == 4 ? k / 4 : (k < kWave ? k : kWave);
-}
-__host__ __device__ inline int bwd_slots_per_wave(int k) {
-  const int s = kWave / bwd_lanes(k);
-  return s < 16 ? s : 16;
-}
-
 __device__ __forceinline__ void lds_add(float* p, float v) {
   // Lowers to ds_add_f32 (no return) for an LDS address. NOTE: ~30x slower than integer
   // LDS atomics on gfx950 (tools/ubench_atomics); kept off the hot paths.
@@ -118,12 +109,16 @@ struct maxk_plan {
   int32_t dim_k = 0;
   const int32_t* src_ptr = nullptr;  // identity of the graph the plan was built for
   const int32_t* src_idx = nullptr;
+  int32_t cus = 256;             // compute units of the device the plan was built on
   // forward
   int32_t fwd_tile_rows = 16;
   int32_t fwd_acc = MAXK_ACC_F64;
   int32_t fwd_rec_bytes = 0;     // packed CBSR record size (k % 4 == 0)
   uint8_t* fwd_rec = nullptr;    // [num_cols][fwd_rec_bytes] workspace (per call pack)
   maxk::FwdTask* fwd_tasks = nullptr;   // e0/e1 index the permuted edge order below
+  int32_t fwd_phases = 1;        // column phases per forward call
+  int32_t fwd_persistent = 0;    // grid = resident capacity (1) or one work-group per task
+  int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per phase
   int32_t* fwd_perm = nullptr;   // CSR edge id of each permuted forward edge
   uint32_t* fwd_cr = nullptr;    // column | (row within the task << 27)
   float* fwd_val = nullptr;      // val snapshot in the permuted order
@@ -132,6 +127,7 @@ struct maxk_plan {
   int32_t n_zero_rows = 0;
   // backward
   int32_t bwd_acc = MAXK_ACC_F64;
+  int32_t bwd_feats = 1;         // features per lane (4: k/4 lanes per edge; 1: k lanes)
   int32_t bwd_block_cols = 0;
   int32_t n_bwd_blocks = 0;
   maxk::BwdTask* bwd_tasks = nullptr;

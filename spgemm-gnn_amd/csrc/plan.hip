@@ -57,6 +57,26 @@ __global__ void fwd_key_kernel(const int32_t* __restrict__ idx, const int32_t* _
   }
 }
 
+// off[t * (B + 1) + b] = first edge of task t whose column is >= b * NC / B (the task's
+// edges are column-sorted).
+__global__ void fwd_phase_kernel(const FwdTask* __restrict__ tasks, int ntasks,
+                                 const uint32_t* __restrict__ cr, int NC, int B,
+                                 int32_t* __restrict__ off) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ntasks * (B + 1)) return;
+  const int t = i / (B + 1), b = i - t * (B + 1);
+  const FwdTask tk = tasks[t];
+  const uint32_t bound = (uint32_t)((int64_t)NC * b / B);
+  int lo = tk.e0, hi = tk.e1;
+  if (b == B) { off[i] = hi; return; }
+  if (b == 0) { off[i] = lo; return; }
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((cr[mid] & ((1u << 27) - 1)) < bound) lo = mid + 1; else hi = mid;
+  }
+  off[i] = lo;
+}
+
 __global__ void gather_fwd_kernel(const int32_t* __restrict__ perm,
                                   const int32_t* __restrict__ idx,
                                   const int32_t* __restrict__ rl_of,
@@ -129,6 +149,7 @@ static void free_plan(maxk_plan* p) {
   dfree(p->fwd_perm);
   dfree(p->fwd_cr);
   dfree(p->fwd_val);
+  dfree(p->fwd_phase_off);
   dfree(p->zero_rows);
   dfree(p->bwd_tasks);
   dfree(p->bwd_perm);
@@ -204,7 +225,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                      o.bwd_accumulator >= 0 && o.bwd_accumulator <= MAXK_ACC_F32_CAS,
                  "maxk_plan_create: unknown accumulator kind");
   MAXK_CHECK_ARG(o.bwd_lds_bytes >= 0 && o.bwd_lds_bytes <= 160 * 1024 &&
-                     o.bwd_tasks_per_cu >= 0 && o.fwd_task_cap >= 0,
+                     o.bwd_tasks_per_cu >= 0 && o.fwd_task_cap >= 0 && o.fwd_phases >= 0 &&
+                     o.fwd_phases <= 64,
                  "maxk_plan_create: bad option value");
   *out_plan = nullptr;
   MAXK_CHECK_ARG(NC >= 0 && (E == 0 || NC > 0), "maxk_plan_create: num_cols out of range");
@@ -224,8 +246,20 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   p->src_ptr = ptr;
   p->src_idx = idx;
   p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
+  {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+        prop.multiProcessorCount > 0)
+      p->cus = prop.multiProcessorCount;
+  }
   p->fwd_acc = o.fwd_accumulator ? o.fwd_accumulator : MAXK_ACC_F64;
   p->bwd_acc = o.bwd_accumulator ? o.bwd_accumulator : MAXK_ACC_F32_CAS;
+  MAXK_CHECK_ARG(o.bwd_features_per_lane == 0 || o.bwd_features_per_lane == 1 ||
+                     (o.bwd_features_per_lane == 4 && k % 4 == 0),
+                 "maxk_plan_create: bwd_features_per_lane must be 0, 1 or 4 (k % 4 == 0)");
+  p->bwd_feats = o.bwd_features_per_lane ? o.bwd_features_per_lane
+                                         : (k % 4 == 0 ? 4 : 1);
 
   int32_t* row_of = nullptr;
   uint32_t* keys_in = nullptr;
@@ -350,6 +384,17 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     PLAN_TRY(hipMemcpyAsync(p->fwd_tasks, ftasks.data(), sizeof(FwdTask) * ftasks.size(),
                             hipMemcpyHostToDevice, s));
     p->device_bytes += sizeof(FwdTask) * ftasks.size();
+    // column phases: enough that one phase's slice of the packed CBSR table is ~L2-sized
+    int B = o.fwd_phases;
+    if (B == 0) B = 1;
+    p->fwd_persistent = o.fwd_persistent ? 1 : 0;
+    B = std::max(1, std::min(B, std::max(NC, 1)));
+    p->fwd_phases = B;
+    PLAN_TRY(hipMalloc(&p->fwd_phase_off, sizeof(int32_t) * nt * (B + 1)));
+    p->device_bytes += sizeof(int32_t) * nt * (B + 1);
+    hipLaunchKernelGGL(fwd_phase_kernel, dim3((nt * (B + 1) + 255) / 256), dim3(256), 0, s,
+                       p->fwd_tasks, nt, p->fwd_cr, NC, B, p->fwd_phase_off);
+    PLAN_TRY(hipGetLastError());
   }
   if (!zrows.empty()) {
     PLAN_TRY(hipMalloc(&p->zero_rows, sizeof(int32_t) * zrows.size()));
@@ -378,7 +423,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     }
   }
   const int lds_budget = o.bwd_lds_bytes ? o.bwd_lds_bytes : kBwdLdsBudget;
-  int C = std::max(1, lds_budget / (k * (int)acc_bytes(p->bwd_acc)));
+  int C = std::max(1, lds_budget / ((k + 1) * (int)acc_bytes(p->bwd_acc)));
   C = std::min(C, std::max(NC, 1));
   const int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
   p->bwd_block_cols = C;

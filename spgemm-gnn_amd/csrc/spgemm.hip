@@ -77,21 +77,38 @@ __global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
   }
 }
 
+// Column phases: all work-groups of one launch gather from the same 1/B of the CBSR table
+// (phase b = source columns [b*NC/B, (b+1)*NC/B)), so the records they touch stay in L2
+// (tools/ubench_gather.hip: ~300 vs ~63 G edges/s for a shared window vs the whole table).
+// Phase 0 stores the task's rows, later phases continue from the stored partial sums.
 template <int VEC, int ACC>
 __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
-    const FwdTask* __restrict__ tasks, const uint32_t* __restrict__ cr,
-    const float* __restrict__ fval, const float* __restrict__ sp_data,
-    const uint8_t* __restrict__ sp_index, const uint8_t* __restrict__ rec, int rec_bytes,
-    float* __restrict__ out, int D, int k, int tile_rows) {
+    const FwdTask* __restrict__ tasks, int ntasks, const int32_t* __restrict__ phase_off,
+    int phases, int phase, const uint32_t* __restrict__ cr, const float* __restrict__ fval,
+    const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
+    const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
+    int tile_rows) {
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
-  const FwdTask t = tasks[blockIdx.x];
+  T* acc = reinterpret_cast<T*>(smem_d);
+  // Work-group w runs tasks w, w + G, ... (G = grid size; G = #tasks by default, or the
+  // resident capacity with the fwd_persistent option, which measured slower on Reddit).
+  for (int ti = blockIdx.x; ti < ntasks; ti += gridDim.x) {
+  FwdTask t = tasks[ti];
+  t.e0 = phase_off[ti * (phases + 1) + phase];
+  t.e1 = phase_off[ti * (phases + 1) + phase + 1];
+  if (phase > 0 && t.e0 == t.e1) continue;  // nothing to add in this phase (uniform)
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
-  T* acc = reinterpret_cast<T*>(smem_d);
   const int n = nrows * D;
-  for (int i = threadIdx.x; i < n; i += kFwdThreads) acc[i] = T(0);
+  __syncthreads();  // the previous task's write-back has finished reading acc
+  if (phase > 0 && !split) {
+    const float* src = out + (size_t)t.row0 * D;
+    for (int i = threadIdx.x; i < n; i += kFwdThreads) acc[i] = T(src[i]);
+  } else {
+    for (int i = threadIdx.x; i < n; i += kFwdThreads) acc[i] = T(0);
+  }
   __syncthreads();
 
   // lanes per edge: VEC==4 => k % 4 == 0 and k/4 <= 64; VEC==1 => min(k, 64) lanes that
@@ -171,6 +188,7 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   } else {
     for (int i = threadIdx.x; i < D; i += kFwdThreads) global_add(dst + i, (float)acc[i]);
   }
+  }  // task loop
 }
 
 __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, float* out,
@@ -197,13 +215,18 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double bsmem[];
-  T* bacc = reinterpret_cast<T*>(bsmem);  // [ncols][k]
+  // Accumulator of column c, feature l at c * KS + pos(l): KS = k + 1 (odd, so different
+  // columns start on different banks) and, with 4 features per lane, feature l = 4q + i at
+  // i * (k / 4) + q, so the k/4 lanes of one edge hit consecutive banks for each i (the
+  // plain [c][k] layout put a wave's 64 lanes on 8 banks: 8-way conflicts on every CAS).
+  T* bacc = reinterpret_cast<T*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
-  const int n = t.ncols * k;
-  for (int i = threadIdx.x; i < n; i += kBwdThreads) bacc[i] = T(0);
+  const int KS = k + 1;
+  const int nacc = t.ncols * KS;
+  for (int i = threadIdx.x; i < nacc; i += kBwdThreads) bacc[i] = T(0);
   __syncthreads();
 
-  const int L = bwd_lanes(k);
+  const int L = (F == 4) ? k / 4 : (k < kWave ? k : kWave);  // lanes per edge
   const int EPS = kWave / L;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
@@ -244,20 +267,33 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (ok[u]) {
-          T* a = bacc + (c[u] - t.col0) * k + q * 4;
+          T* a = bacc + (c[u] - t.col0) * KS + q;
           A::add(a, v[u] * g[u][0]);
-          A::add(a + 1, v[u] * g[u][1]);
-          A::add(a + 2, v[u] * g[u][2]);
-          A::add(a + 3, v[u] * g[u][3]);
+          A::add(a + L, v[u] * g[u][1]);
+          A::add(a + 2 * L, v[u] * g[u][2]);
+          A::add(a + 3 * L, v[u] * g[u][3]);
         }
       }
+    } else if (k <= kWave) {
+      // one feature per lane: the L = k lanes of an edge read k dwords of the same
+      // grad_out row in one instruction (~7 cache lines at k = 16 instead of 16 for 4
+      // features per lane over 4 instructions); the gather is bound by lines per request.
+      uint32_t sel[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) sel[u] = sp_index[(size_t)c[u] * k + q];
+      float g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) g[u] = G[(size_t)r[u] * D + sel[u]];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (ok[u]) A::add(bacc + (c[u] - t.col0) * KS + q, v[u] * g[u]);
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (ok[u]) {
           const float* grow = G + (size_t)r[u] * D;
           const uint8_t* srow = sp_index + (size_t)c[u] * k;
-          T* a = bacc + (c[u] - t.col0) * k;
+          T* a = bacc + (c[u] - t.col0) * KS;
           for (int l = q; l < k; l += L) A::add(a + l, v[u] * grow[srow[l]]);
         }
       }
@@ -266,10 +302,13 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
   __syncthreads();
 
   float* dst = grad_sp + (size_t)t.col0 * k;
-  if (t.shared) {
-    for (int i = threadIdx.x; i < n; i += kBwdThreads) global_add(dst + i, (float)bacc[i]);
-  } else {
-    for (int i = threadIdx.x; i < n; i += kBwdThreads) dst[i] = (float)bacc[i];
+  const int n = t.ncols * k;
+  for (int i = threadIdx.x; i < n; i += kBwdThreads) {
+    const int cl = i / k;
+    const int l = i - cl * k;
+    const int pos = cl * KS + (F == 4 ? (l & 3) * (k >> 2) + (l >> 2) : l);
+    if (t.shared) global_add(dst + i, (float)bacc[pos]);
+    else dst[i] = (float)bacc[pos];
   }
 }
 
@@ -305,7 +344,7 @@ size_t fwd_lds_bytes(int tile_rows, int D, int acc) {
 }
 
 size_t bwd_lds_bytes(int block_cols, int k, int acc) {
-  return (size_t)block_cols * k * acc_bytes(acc);
+  return (size_t)block_cols * (k + 1) * acc_bytes(acc);
 }
 
 template <typename K>
@@ -349,6 +388,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
     MAXK_LAUNCH_CHECK("zero_rows launch");
   }
   const int R = plan->fwd_tile_rows;
+  const int B = plan->fwd_phases;
   const size_t lds = fwd_lds_bytes(R, D, plan->fwd_acc);
   const int rec_bytes = plan->fwd_rec_bytes;
   if (k % 4 == 0 && plan->num_cols > 0) {
@@ -358,13 +398,22 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
                        plan->fwd_rec, plan->num_cols, k, rec_bytes);
     MAXK_LAUNCH_CHECK("pack_cbsr launch");
   }
-  const dim3 grid(plan->n_fwd_tasks), block(kFwdThreads);
+  const dim3 block(kFwdThreads);
+  // persistent grid: as many work-groups as fit on the device at once (capped by tasks)
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \
     if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, A>, lds));          \
-    hipLaunchKernelGGL((spgemm_fwd_kernel<V, A>), grid, block, lds, s, plan->fwd_tasks,      \
-                       plan->fwd_cr, plan->fwd_val, sp_data, sp_index, plan->fwd_rec,      \
-                       rec_bytes, out, D, k, R);                                           \
+    int per_cu = 0;                                                                       \
+    MAXK_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(                            \
+        &per_cu, spgemm_fwd_kernel<V, A>, kFwdThreads, lds));                             \
+    const int g = plan->fwd_persistent                                                    \
+                      ? std::max(1, std::min(plan->n_fwd_tasks, std::max(per_cu, 1) * plan->cus)) \
+                      : plan->n_fwd_tasks;                                                \
+    for (int b = 0; b < B; ++b)                                                           \
+      hipLaunchKernelGGL((spgemm_fwd_kernel<V, A>), dim3(g), block, lds, s, plan->fwd_tasks, \
+                         plan->n_fwd_tasks, plan->fwd_phase_off, B, b, plan->fwd_cr,       \
+                         plan->fwd_val, sp_data, sp_index, plan->fwd_rec, rec_bytes, out,  \
+                         D, k, R);                                                         \
   } while (0)
   if (k % 4 == 0) {
     if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(4, MAXK_ACC_F32_CAS);
@@ -404,7 +453,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
                        plan->bwd_row, plan->bwd_col, plan->bwd_val, grad_out, sp_index,   \
                        grad_sp, D, k);                                                    \
   } while (0)
-  if (bwd_feats(k) == 4) {
+  if (plan->bwd_feats == 4) {
     if (plan->bwd_acc == MAXK_ACC_F32_CAS) BWD_LAUNCH(4, MAXK_ACC_F32_CAS);
     else BWD_LAUNCH(4, MAXK_ACC_F64);
   } else {

@@ -53,7 +53,10 @@ class PlanOptions(ctypes.Structure):
         ("bwd_accumulator", _i32),
         ("bwd_tasks_per_cu", _i32),
         ("fwd_task_cap", _i32),
-        ("reserved", _i32 * 2),
+        ("bwd_features_per_lane", _i32),
+        ("fwd_phases", _i32),
+        ("fwd_persistent", _i32),
+        ("reserved", _i32 * 3),
     ]
 
 

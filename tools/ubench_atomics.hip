@@ -123,9 +123,9 @@ __global__ __launch_bounds__(512) void bwd_kern(const int4* __restrict__ tasks,
     float g[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float* gr = G + (size_t)r[u] * D;
+      const float* gr = G + (size_t)(V == 5 ? (r[u] & 255) : r[u]) * D;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) g[u][j] = gr[(s[u] >> (8 * j)) & 0xff];
+      for (int j = 0; j < 4; ++j) g[u][j] = (V == 6) ? v[u] * (float)j : gr[(s[u] >> (8 * j)) & 0xff];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(512) void bwd_kern(const int4* __restrict__ tasks,
         for (int j = 0; j < 4; ++j) {
           if (V == 0) __hip_atomic_fetch_add(a + j * L, v[u] * g[u][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           else if (V == 1) a[j * L] += v[u] * g[u][j];
-          else if (V == 3) lds_add_cas(a + j * L, v[u] * g[u][j]);
+          else if (V == 3 || V == 5 || V == 6) lds_add_cas(a + j * L, v[u] * g[u][j]);
           else if (V == 4) __hip_atomic_fetch_add(accd + (c[u] - t.x) * KS + q + j * L, (double)(v[u] * g[u][j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           else reg += v[u] * g[u][j];
         }
@@ -159,12 +159,16 @@ extern "C" float ubench_bwd(int variant, const int4* tasks, int ntasks, const in
   (void)hipFuncSetAttribute((const void*)bwd_kern<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)bwd_kern<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)bwd_kern<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)bwd_kern<5>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)bwd_kern<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   auto launch = [&]() {
     if (variant == 0) hipLaunchKernelGGL(bwd_kern<0>, ntasks, 512, lds, 0, tasks, erow, ecol, ev, G, sp_index, grad, D);
     if (variant == 1) hipLaunchKernelGGL(bwd_kern<1>, ntasks, 512, lds, 0, tasks, erow, ecol, ev, G, sp_index, grad, D);
     if (variant == 2) hipLaunchKernelGGL(bwd_kern<2>, ntasks, 512, lds, 0, tasks, erow, ecol, ev, G, sp_index, grad, D);
     if (variant == 3) hipLaunchKernelGGL(bwd_kern<3>, ntasks, 512, lds, 0, tasks, erow, ecol, ev, G, sp_index, grad, D);
     if (variant == 4) hipLaunchKernelGGL(bwd_kern<4>, ntasks, 512, lds, 0, tasks, erow, ecol, ev, G, sp_index, grad, D);
+    if (variant == 5) hipLaunchKernelGGL(bwd_kern<5>, ntasks, 512, lds, 0, tasks, erow, ecol, ev, G, sp_index, grad, D);
+    if (variant == 6) hipLaunchKernelGGL(bwd_kern<6>, ntasks, 512, lds, 0, tasks, erow, ecol, ev, G, sp_index, grad, D);
   };
   launch();
   (void)hipEventRecord(a, 0);

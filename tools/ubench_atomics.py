@@ -22,7 +22,7 @@ out = torch.empty(NWG * 256, device=dev)
 adds = NWG * 256 * 256 * 4
 names = ["ds_add_f32", "ds_add_u32", "ds_add_u64", "ds_add_f64", "ds RMW (racy)",
          "global f32 atomic agent", "global f32 atomic workgroup", "global store", "LDS f32 CAS add"]
-for v in (0, 1, 2, 3, 4, 8):
+for v in ():
     ms = lib.ubench_atomics(v, table.data_ptr(), table.numel(), out.data_ptr(), NWG, 3)
     print(f"{v} {names[v]:30s} {ms:8.3f} ms  {adds / ms / 1e6:9.2f} G adds/s", flush=True)
 
@@ -33,7 +33,7 @@ val = graphs.sage_mean_values(ptr)
 rows = torch.repeat_interleave(torch.arange(N, device=dev), (ptr[1:] - ptr[:-1]).long())
 G = torch.randn(N, 256, device=dev)
 sp_index = torch.sort(torch.randint(0, 256, (N, 16), device=dev, dtype=torch.int32), 1).values.to(torch.uint8)
-for C in (960, 1200, 1920, 2400):
+for C in (2400,):
     key = (idx.long() // C) * N + rows
     order = torch.argsort(key)
     erow, ecol, ev = rows[order].int().contiguous(), idx.long()[order].int().contiguous(), val[order].contiguous()
@@ -49,7 +49,7 @@ for C in (960, 1200, 1920, 2400):
             tasks.append([blk * C, min(C, N - blk * C), e0, e1])
     tasks_t = torch.tensor(tasks, dtype=torch.int32, device=dev).contiguous()
     grad = torch.empty(N * 16, device=dev)
-    for v, nm in [(1, "racy RMW"), (3, "f32 CAS"), (4, "f64 atomic")]:
+    for v, nm in [(3, "f32 CAS"), (5, "CAS, hot G"), (6, "CAS, no G"), (1, "racy RMW")]:
         lds = C * 16 * 4 * (2 if v == 4 else 1)
         if lds > 160 * 1024:
             continue

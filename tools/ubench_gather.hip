@@ -24,13 +24,16 @@ __global__ __launch_bounds__(256) void gkern(const int* __restrict__ idx,
   const int e0 = blockIdx.x * edges_per_wg;
   float accv = 0.f;
   uint32_t accs = 0;
-  const int wbase = (V == 3 || V == 4) ? (blockIdx.x * 7919) % (232965 - window) : 0;
+  // window > 0: per-WG window at a WG-specific offset; window < 0: one global window
+  // [0, -window) shared by every work-group (L2-resident for all of them)
+  const int wabs = window < 0 ? -window : window;
+  const int wbase = (V == 3 || V == 4) && window > 0 ? (blockIdx.x * 7919) % (232965 - wabs) : 0;
   for (int base = wave * EPS * U; base < edges_per_wg; base += 4 * EPS * U) {
     int c[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       c[u] = idx[e0 + base + u * EPS + slot];
-      if (V == 3 || V == 4) c[u] = wbase + c[u] % window;
+      if (V == 3 || V == 4) c[u] = wbase + c[u] % wabs;
     }
     float4 x[U];
     uint32_t s[U];
