@@ -17,7 +17,8 @@ constexpr int kFwdThreads = 256;        // 4 waves
 constexpr int kBwdThreads = 512;        // 8 waves
 constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
 constexpr int kFwdUnroll = 8;           // independent sub-steps in flight per wave
-constexpr int kBwdUnroll = 8;
+constexpr int kBwdUnroll = 16;
+constexpr int kBwdTasksPerCu = 8;
 constexpr int kBwdLdsBudget = 150 * 1024; // one 512-thread work-group per CU
 
 // Thread-local error message plumbing for maxk_last_error().
@@ -118,6 +119,8 @@ struct maxk_plan {
   maxk::FwdTask* fwd_tasks = nullptr;   // e0/e1 index the permuted edge order below
   int32_t fwd_phases = 1;        // column phases per forward call
   int32_t fwd_persistent = 0;    // grid = resident capacity (1) or one work-group per task
+  int32_t fwd_unroll = 8;        // independent sub-steps per wave (8 or 16)
+  int32_t bwd_unroll = 8;
   int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per phase
   int32_t* fwd_perm = nullptr;   // CSR edge id of each permuted forward edge
   uint32_t* fwd_cr = nullptr;    // column | (row within the task << 27)

@@ -246,6 +246,11 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   p->src_ptr = ptr;
   p->src_idx = idx;
   p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
+  MAXK_CHECK_ARG((o.fwd_unroll == 0 || o.fwd_unroll == 8 || o.fwd_unroll == 16) &&
+                     (o.bwd_unroll == 0 || o.bwd_unroll == 8 || o.bwd_unroll == 16),
+                 "maxk_plan_create: unroll must be 0, 8 or 16");
+  p->fwd_unroll = o.fwd_unroll ? o.fwd_unroll : kFwdUnroll;
+  p->bwd_unroll = o.bwd_unroll ? o.bwd_unroll : kBwdUnroll;
   {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -473,7 +478,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     }
     for (int b = 0; b <= nblocks; ++b) offs[b] = offs32[b];
   }
-  const int64_t target_tasks = (int64_t)(o.bwd_tasks_per_cu ? o.bwd_tasks_per_cu : 4) * cus;
+  const int64_t target_tasks = (int64_t)(o.bwd_tasks_per_cu ? o.bwd_tasks_per_cu : kBwdTasksPerCu) * cus;
   const int chunks = (int)std::max<int64_t>(1, (target_tasks + nblocks - 1) / std::max(nblocks, 1));
   std::vector<BwdTask> btasks;
   int nshared = 0;

@@ -81,7 +81,7 @@ __global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
 // (phase b = source columns [b*NC/B, (b+1)*NC/B)), so the records they touch stay in L2
 // (tools/ubench_gather.hip: ~300 vs ~63 G edges/s for a shared window vs the whole table).
 // Phase 0 stores the task's rows, later phases continue from the stored partial sums.
-template <int VEC, int ACC>
+template <int VEC, int ACC, int U>
 __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     const FwdTask* __restrict__ tasks, int ntasks, const int32_t* __restrict__ phase_off,
     int phases, int phase, const uint32_t* __restrict__ cr, const float* __restrict__ fval,
@@ -128,7 +128,6 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     // chain (col, val) -> CBSR record -> LDS has two dependent global round trips, so
     // memory-level parallelism comes from U independent sub-steps per wave. Out-of-range
     // lanes load a clamped (valid) edge and skip the update.
-    constexpr int U = kFwdUnroll;
     const int last = t.e1 - 1;
     for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
       uint32_t cw[U];
@@ -206,7 +205,7 @@ __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, fl
 // instruction covers share few rows of grad_out, so its gathers stay in the CU's L1. Any
 // wave may update any column of the block (that is what keeps the row locality), hence the
 // atomic LDS accumulation.
-template <int F, int ACC>
+template <int F, int ACC, int U>
 __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
     const BwdTask* __restrict__ tasks, const int32_t* __restrict__ erow,
     const int32_t* __restrict__ ecol, const float* __restrict__ evals,
@@ -215,10 +214,9 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double bsmem[];
-  // Accumulator of column c, feature l at c * KS + pos(l): KS = k + 1 (odd, so different
-  // columns start on different banks) and, with 4 features per lane, feature l = 4q + i at
-  // i * (k / 4) + q, so the k/4 lanes of one edge hit consecutive banks for each i (the
-  // plain [c][k] layout put a wave's 64 lanes on 8 banks: 8-way conflicts on every CAS).
+  // Accumulator of column c, slot l at c * KS + l with KS = k + 1 (odd, so different columns
+  // start on different banks); the lanes of one edge update consecutive slots (the plain
+  // [c][k] layout with lane-contiguous slots put a wave on 8 banks: 8-way conflicts).
   T* bacc = reinterpret_cast<T*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
   const int KS = k + 1;
@@ -234,7 +232,6 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
   const int q = lane - slot * L;
   const bool lane_on = slot < EPS;
   constexpr int kWaves = kBwdThreads / kWave;
-  constexpr int U = kBwdUnroll;
   const int last = t.e1 - 1;
 
   for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
@@ -251,10 +248,23 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
       v[u] = evals[ec];
     }
     if constexpr (F == 4) {
+      // Lane q of an edge owns the selector slots q, q + L, q + 2L, q + 3L: in gather
+      // instruction i the L lanes of the edge read L adjacent (sorted) selectors of the
+      // row, i.e. ~1-2 cache lines of grad_out[r] instead of L lines. The selector words
+      // are loaded as dwords (lane q: slots 4q..4q+3) and redistributed with shuffles.
       uint32_t sel[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        sel[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)c[u] * k + q * 4);
+      for (int u = 0; u < U; ++u) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)c[u] * k + q * 4);
+        uint32_t m = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int l = q + L * i;  // slot owned by this lane in gather i
+          const uint32_t wi = (uint32_t)__shfl((int)w, slot * L + (l >> 2), kWave);
+          m |= ((wi >> ((l & 3) * 8)) & 0xffu) << (8 * i);
+        }
+        sel[u] = m;
+      }
       float g[U][4];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -306,7 +316,7 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
   for (int i = threadIdx.x; i < n; i += kBwdThreads) {
     const int cl = i / k;
     const int l = i - cl * k;
-    const int pos = cl * KS + (F == 4 ? (l & 3) * (k >> 2) + (l >> 2) : l);
+    const int pos = cl * KS + l;
     if (t.shared) global_add(dst + i, (float)bacc[pos]);
     else dst[i] = (float)bacc[pos];
   }
@@ -400,20 +410,25 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
   }
   const dim3 block(kFwdThreads);
   // persistent grid: as many work-groups as fit on the device at once (capped by tasks)
-#define FWD_LAUNCH(V, A)                                                                  \
+#define FWD_LAUNCH1(V, A, UU)                                                             \
   do {                                                                                    \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, A>, lds));          \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, A, UU>, lds));      \
     int per_cu = 0;                                                                       \
     MAXK_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(                            \
-        &per_cu, spgemm_fwd_kernel<V, A>, kFwdThreads, lds));                             \
+        &per_cu, spgemm_fwd_kernel<V, A, UU>, kFwdThreads, lds));                         \
     const int g = plan->fwd_persistent                                                    \
                       ? std::max(1, std::min(plan->n_fwd_tasks, std::max(per_cu, 1) * plan->cus)) \
                       : plan->n_fwd_tasks;                                                \
     for (int b = 0; b < B; ++b)                                                           \
-      hipLaunchKernelGGL((spgemm_fwd_kernel<V, A>), dim3(g), block, lds, s, plan->fwd_tasks, \
+      hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU>), dim3(g), block, lds, s, plan->fwd_tasks, \
                          plan->n_fwd_tasks, plan->fwd_phase_off, B, b, plan->fwd_cr,       \
                          plan->fwd_val, sp_data, sp_index, plan->fwd_rec, rec_bytes, out,  \
                          D, k, R);                                                         \
+  } while (0)
+#define FWD_LAUNCH(V, A)                                                                  \
+  do {                                                                                    \
+    if (plan->fwd_unroll == 16) FWD_LAUNCH1(V, A, 16);                                    \
+    else FWD_LAUNCH1(V, A, 8);                                                            \
   } while (0)
   if (k % 4 == 0) {
     if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(4, MAXK_ACC_F32_CAS);
@@ -423,6 +438,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
     else FWD_LAUNCH(1, MAXK_ACC_F64);
   }
 #undef FWD_LAUNCH
+#undef FWD_LAUNCH1
   MAXK_LAUNCH_CHECK("spgemm_fwd launch");
   return MAXK_OK;
 }
@@ -446,12 +462,17 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   if (plan->n_bwd_tasks == 0) return MAXK_OK;
   const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k, plan->bwd_acc);
   const dim3 grid(plan->n_bwd_tasks), block(kBwdThreads);
-#define BWD_LAUNCH(F, A)                                                                  \
+#define BWD_LAUNCH1(F, A, UU)                                                             \
   do {                                                                                    \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd_kernel<F, A>, lds));           \
-    hipLaunchKernelGGL((sspmm_bwd_kernel<F, A>), grid, block, lds, s, plan->bwd_tasks,    \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd_kernel<F, A, UU>, lds));       \
+    hipLaunchKernelGGL((sspmm_bwd_kernel<F, A, UU>), grid, block, lds, s, plan->bwd_tasks, \
                        plan->bwd_row, plan->bwd_col, plan->bwd_val, grad_out, sp_index,   \
                        grad_sp, D, k);                                                    \
+  } while (0)
+#define BWD_LAUNCH(F, A)                                                                  \
+  do {                                                                                    \
+    if (plan->bwd_unroll == 16) BWD_LAUNCH1(F, A, 16);                                    \
+    else BWD_LAUNCH1(F, A, 8);                                                            \
   } while (0)
   if (plan->bwd_feats == 4) {
     if (plan->bwd_acc == MAXK_ACC_F32_CAS) BWD_LAUNCH(4, MAXK_ACC_F32_CAS);
@@ -461,6 +482,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     else BWD_LAUNCH(1, MAXK_ACC_F64);
   }
 #undef BWD_LAUNCH
+#undef BWD_LAUNCH1
   MAXK_LAUNCH_CHECK("sspmm_bwd launch");
   return MAXK_OK;
 }

@@ -56,7 +56,9 @@ class PlanOptions(ctypes.Structure):
         ("bwd_features_per_lane", _i32),
         ("fwd_phases", _i32),
         ("fwd_persistent", _i32),
-        ("reserved", _i32 * 3),
+        ("fwd_unroll", _i32),
+        ("bwd_unroll", _i32),
+        ("reserved", _i32 * 1),
     ]
 
 

@@ -52,10 +52,10 @@ def main():
     sp_data, sp_index = mk.maxk_forward(h, args.k, return_index=True)
     del h
 
-    fwd_variants = [dict()] + [dict(fwd_tile_rows=r, fwd_phases=b, fwd_accumulator=a)
-                               for r, b, a in itertools.product((16, 32), (1, 2), ("f64", "f32_cas"))]
-    bwd_variants = [dict()] + [dict(bwd_accumulator=a, bwd_tasks_per_cu=t)
-                               for a, t in itertools.product(("f64", "f32_cas"), (2, 4, 8))]
+    fwd_variants = [dict()] + [dict(fwd_tile_rows=r, fwd_unroll=u)
+                               for r, u in itertools.product((16, 32), (8, 16))]
+    bwd_variants = [dict()] + [dict(bwd_unroll=u, bwd_tasks_per_cu=t, bwd_lds_bytes=b)
+                               for u, t, b in itertools.product((8, 16), (4, 8), (76800, 153600))]
     ref_out = ref_grad = None
     results = []
     if args.which in ("fwd", "both"):
