@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-comparator", action="store_true")
+    ap.add_argument("--k-sweep", default="8,32,64",
+                    help="extra k values timed at N=1 (kernel device time; '' to skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -277,6 +279,35 @@ def main():
         "plan_build_s": plan_s,
         "cpu_baseline": None,
     }
+
+    if world == 1 and args.k_sweep:
+        # the metric's k in {8,16,32,64}: same graph and features, kernel device time only
+        sweep = {str(k): {"fwd_ms": fwd_ms, "bwd_ms": bwd_ms,
+                          "edges_per_s": 2 * e / ((fwd_ms + bwd_ms) * 1e-3),
+                          "fwd_roofline_frac": fwd_gbs / HBM_PEAK_GBS,
+                          "bwd_roofline_frac": bwd_gbs / HBM_PEAK_GBS}}
+        h_full = graphs.features(n, d, seed=97, device=dev)
+        for ks in [int(x) for x in args.k_sweep.split(",") if x.strip()]:
+            if ks == k:
+                continue
+            sd, si = mk.maxk_forward(h_full, ks, return_index=True)
+            p = mk.GraphPlan(ptr, idx, val, n, e, d, ks)
+            o = torch.empty((n, d), dtype=torch.float32, device=dev)
+            gr = torch.empty((n, ks), dtype=torch.float32, device=dev)
+            for _ in range(2):
+                p.forward(sd, si, o)
+                p.backward(g, si, gr)
+            tf = event_time_ms(lambda: p.forward(sd, si, o), reps)
+            tb = event_time_ms(lambda: p.backward(g, si, gr), reps)
+            sweep[str(ks)] = {
+                "fwd_ms": tf, "bwd_ms": tb, "edges_per_s": 2 * e / ((tf + tb) * 1e-3),
+                "fwd_roofline_frac": fwd_bytes(n, e, ks, d) / (tf * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "bwd_roofline_frac": bwd_bytes(n, e, ks, d) / (tb * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            }
+            log(f"k={ks}: fwd {tf:.3f} ms bwd {tb:.3f} ms")
+            del p, sd, si, o, gr
+        del h_full
+        result["k_sweep"] = dict(sorted(sweep.items(), key=lambda kv: int(kv[0])))
 
     if rank == 0 and world == 1 and not args.no_comparator:
         # rocSPARSE CSR SpMM on the dense MaxK output (the reference's cuSPARSE comparator,

@@ -21,7 +21,7 @@ for s in $STEPS; do
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats \
         -d "$OUT/prof" -o bench --output-format csv -- \
-        python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-comparator ${BENCH_ARGS} \
+        python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-comparator --k-sweep "" ${BENCH_ARGS} \
         > "$OUT/prof_bench.json" 2> "$OUT/prof.log"); rc=$?
       tail -3 "$OUT/prof.log"; [ $rc -eq 0 ] || exit $rc
       find "$OUT/prof" -name "*kernel_stats.csv" | head -3 ;;

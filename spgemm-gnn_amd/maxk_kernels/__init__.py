@@ -29,15 +29,19 @@ from .autograd import (  # noqa: F401
     CSRGraph,
     MaxKFunction,
     SpGEMMFunction,
+    densify,
     maxk,
     maxk_aggregate,
     spgemm,
 )
 
+from .layers import MaxKGCN, MaxKGCNConv, MaxKSAGE, MaxKSAGEConv  # noqa: F401,E402
+
 __all__ = [
     "maxk_forward", "maxk_backward", "spgemm_forward", "spgemm_backward",
     "dense_spmm", "GraphPlan", "get_plan", "clear_plan_cache", "CSRGraph",
     "MaxKFunction", "SpGEMMFunction", "maxk", "spgemm", "maxk_aggregate", "MaxKError",
+    "densify", "MaxKSAGEConv", "MaxKGCNConv", "MaxKSAGE", "MaxKGCN",
 ]
 
 ABI_VERSION = lib.maxk_abi_version()

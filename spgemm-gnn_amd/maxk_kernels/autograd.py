@@ -14,7 +14,7 @@ module that does not exist) and its ``MaxKFunction`` (utils/maxk_layers.py:16-45
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
@@ -28,11 +28,21 @@ class CSRGraph:
 
     This is ``A`` in ``Y = A X``; for DGL's ``update_all(copy_u, ...)`` it is the CSR of
     the in-edges (row = destination node), i.e. ``g.adj_tensors('csc')`` of a DGL graph.
+    (The reference takes ``adj_tensors('csr')``, the out-edge CSR, at
+    utils/maxk_layers.py:106 — correct only for symmetric graphs; SURVEY §8(b) defect 5.)
     """
 
     ptr: torch.Tensor
     idx: torch.Tensor
-    val: torch.Tensor
+    val: Optional[torch.Tensor] = None
+    _values: dict = field(default_factory=dict, repr=False, compare=False)
+
+    def __post_init__(self):
+        self.ptr = self.ptr.to(torch.int32).contiguous()
+        self.idx = self.idx.to(torch.int32).contiguous()
+        if self.val is None:
+            self.val = torch.ones(self.idx.numel(), dtype=torch.float32, device=self.idx.device)
+        self.val = self.val.to(torch.float32).contiguous()
 
     @property
     def num_nodes(self) -> int:
@@ -42,9 +52,89 @@ class CSRGraph:
     def num_edges(self) -> int:
         return self.idx.numel()
 
+    @property
+    def device(self) -> torch.device:
+        return self.ptr.device
+
     def plan(self, dim_origin: int, dim_k: int) -> ops.GraphPlan:
         return ops.get_plan(self.ptr, self.idx, self.val, self.num_nodes, self.num_edges,
                             dim_origin, dim_k)
+
+    # -- construction -----------------------------------------------------------------
+    @classmethod
+    def from_edges(cls, src: torch.Tensor, dst: torch.Tensor, num_nodes: int,
+                   val: Optional[torch.Tensor] = None) -> "CSRGraph":
+        """Edges u -> v (messages flow src -> dst), grouped by destination row."""
+        src, dst = src.to(torch.int64), dst.to(torch.int64)
+        key = dst * num_nodes + src
+        order = torch.argsort(key, stable=True)
+        cnt = torch.bincount(dst, minlength=num_nodes)
+        ptr = torch.zeros(num_nodes + 1, dtype=torch.int64, device=src.device)
+        ptr[1:] = torch.cumsum(cnt, 0)
+        return cls(ptr, src[order], None if val is None else val[order])
+
+    @classmethod
+    def from_dgl(cls, g) -> "CSRGraph":
+        """In-edge CSR of a homogeneous DGL graph (``adj_tensors('csc')``: indptr over
+        destinations, indices = sources). Cached on the graph object."""
+        cached = getattr(g, "_maxk_csr", None)
+        if isinstance(cached, CSRGraph):
+            return cached
+        indptr, indices, _ = g.adj_tensors("csc")
+        csr = cls(indptr, indices)
+        try:
+            g._maxk_csr = csr
+        except AttributeError:  # pragma: no cover - frozen graph objects
+            pass
+        return csr
+
+    # -- degrees and edge weights -----------------------------------------------------
+    def in_degrees(self) -> torch.Tensor:
+        return (self.ptr[1:] - self.ptr[:-1]).to(torch.int64)
+
+    def out_degrees(self) -> torch.Tensor:
+        return torch.bincount(self.idx.to(torch.int64), minlength=self.num_nodes)
+
+    def edge_values(self, kind: str) -> torch.Tensor:
+        """Per-edge weights for the aggregation ``kind`` (cached):
+
+        * ``"sum"`` / ``"none"``: 1
+        * ``"mean"`` / ``"right"``: 1 / in_deg(dst)   (DGL fn.mean, GraphConv norm='right')
+        * ``"left"``: 1 / out_deg(src)
+        * ``"both"``: out_deg(src)^-1/2 * in_deg(dst)^-1/2   (GraphConv norm='both')
+
+        Degrees are clamped to >= 1 (utils/maxk_layers.py:148,302,371).
+        """
+        v = self._values.get(kind)
+        if v is not None:
+            return v
+        rows = torch.repeat_interleave(torch.arange(self.num_nodes, device=self.device),
+                                       self.in_degrees())
+        cols = self.idx.to(torch.int64)
+        ind = self.in_degrees().clamp(min=1).to(torch.float32)
+        outd = self.out_degrees().clamp(min=1).to(torch.float32)
+        if kind in ("sum", "none"):
+            v = torch.ones(self.num_edges, dtype=torch.float32, device=self.device)
+        elif kind in ("mean", "right"):
+            v = (1.0 / ind)[rows]
+        elif kind == "left":
+            v = (1.0 / outd)[cols]
+        elif kind == "both":
+            v = outd.rsqrt()[cols] * ind.rsqrt()[rows]
+        else:
+            raise ValueError(f"unknown aggregation weights {kind!r}")
+        v = v.contiguous()
+        self._values[kind] = v
+        return v
+
+    def with_values(self, kind: str) -> "CSRGraph":
+        """Same structure with the ``kind`` edge weights (shares ptr/idx, hence the plan)."""
+        key = ("graph", kind)
+        g = self._values.get(key)
+        if g is None:
+            g = CSRGraph(self.ptr, self.idx, self.edge_values(kind))
+            self._values[key] = g
+        return g
 
 
 class MaxKFunction(torch.autograd.Function):
@@ -90,6 +180,14 @@ class SpGEMMFunction(torch.autograd.Function):
                                           graph.num_edges, k, dim_origin,
                                           plan=graph.plan(dim_origin, k))
         return grad_sp, None, None, None
+
+
+def densify(sp_data: torch.Tensor, sp_index: torch.Tensor, dim_origin: int) -> torch.Tensor:
+    """Dense ``[N, D]`` view of CBSR features (differentiable in sp_data; duplicate
+    selectors sum, as in the kernels)."""
+    out = torch.zeros((sp_data.shape[0], dim_origin), dtype=sp_data.dtype,
+                      device=sp_data.device)
+    return out.scatter_add(1, sp_index.long(), sp_data)
 
 
 def maxk(x: torch.Tensor, k: int, mode: str = "exact"):

@@ -1,5 +1,7 @@
-"""GPU, BASELINE full size (Reddit-shaped synthetic graph, D=256, k=16): parity through
-size-independent properties plus sampled rows/columns checked against the oracle.
+"""GPU, BASELINE.json full sizes (synthetic graphs with the datasets' N and E, D=256):
+parity through size-independent properties plus sampled rows/columns checked against
+the oracle. Cases follow BASELINE.json configs: Reddit SAGE-mean k=16 (the bench
+workload) and k=8/64, ogbn-products SAGE k=32, ogbn-proteins GCN k in {8,16,32,64}.
 
 * adjoint identity   <A densify(sp), G> == <sp_data, SSpMM(G)>   (float64 reductions)
 * linearity          SpGEMM(2 sp_data) == 2 SpGEMM(sp_data)
@@ -16,27 +18,41 @@ from oracle import oracle
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
-N, E = graphs.DATASETS["reddit"]
-D, K = 256, 16
+D = 256
+CASES = [("reddit", "sage", 16), ("reddit", "sage", 8), ("reddit", "sage", 64),
+         ("ogbn-products", "sage", 32),
+         ("ogbn-proteins", "gcn", 8), ("ogbn-proteins", "gcn", 16),
+         ("ogbn-proteins", "gcn", 32), ("ogbn-proteins", "gcn", 64)]
+_GRAPHS = {}
 
 
-@pytest.fixture(scope="module")
-def reddit(gpu):
-    ptr, idx = graphs.synthetic_csr(N, E, seed=97, device=gpu)
-    val = graphs.sage_mean_values(ptr)
-    h = graphs.features(N, D, seed=97, device=gpu)
-    g = graphs.features(N, D, seed=98, device=gpu)
-    sp_data, sp_index = mk.maxk_forward(h, K, return_index=True)
-    return ptr, idx, val, sp_data, sp_index, g
+@pytest.fixture(scope="module", params=CASES, ids=lambda c: f"{c[0]}-{c[1]}-k{c[2]}")
+def case(request, gpu):
+    name, kind, k = request.param
+    if (name, kind) not in _GRAPHS:
+        _GRAPHS.clear()   # one full-size graph resident at a time
+        torch.cuda.empty_cache()
+        n, e = graphs.DATASETS[name]
+        ptr, idx = graphs.synthetic_csr(n, e, seed=97, device=gpu)
+        val = graphs.sage_mean_values(ptr) if kind == "sage" else graphs.gcn_values(ptr, idx)
+        h = graphs.features(n, D, seed=97, device=gpu)
+        g = graphs.features(n, D, seed=98, device=gpu)
+        _GRAPHS[(name, kind)] = (ptr, idx, val, h, g)
+    ptr, idx, val, h, g = _GRAPHS[(name, kind)]
+    sp_data, sp_index = mk.maxk_forward(h, k, return_index=True)
+    mk.clear_plan_cache()
+    return ptr, idx, val, sp_data, sp_index, g, name, k
 
 
-def test_graph_shape(reddit):
-    ptr, idx = reddit[0], reddit[1]
-    assert ptr.numel() == N + 1 and idx.numel() == E and int(ptr[-1]) == E
+def test_graph_shape(case):
+    ptr, idx, name = case[0], case[1], case[6]
+    n, e = graphs.DATASETS[name]
+    assert ptr.numel() == n + 1 and idx.numel() == e and int(ptr[-1]) == e
 
 
-def test_adjoint_and_linearity(reddit):
-    ptr, idx, val, sp_data, sp_index, g = reddit
+def test_adjoint_and_linearity(case):
+    ptr, idx, val, sp_data, sp_index, g, _, K = case
+    N, E = ptr.numel() - 1, idx.numel()
     y, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, N, E, K, D)
     gs = mk.spgemm_backward(ptr, idx, val, g, sp_index, N, E, K, D)
     lhs = (y.double() * g.double()).sum().item()
@@ -48,8 +64,9 @@ def test_adjoint_and_linearity(reddit):
     assert ((y2.double() - 2 * y.double()).abs() <= 1e-5 * mag + 1e-30).all()
 
 
-def test_sampled_rows_vs_oracle(reddit):
-    ptr, idx, val, sp_data, sp_index, _ = reddit
+def test_sampled_rows_vs_oracle(case):
+    ptr, idx, val, sp_data, sp_index, _, _, K = case
+    N, E = ptr.numel() - 1, idx.numel()
     y, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, N, E, K, D)
     p = ptr.cpu().numpy()
     deg = np.diff(p)
@@ -71,8 +88,9 @@ def test_sampled_rows_vs_oracle(reddit):
     assert ok, worst
 
 
-def test_sampled_columns_vs_oracle(reddit):
-    ptr, idx, val, _, sp_index, g = reddit
+def test_sampled_columns_vs_oracle(case):
+    ptr, idx, val, _, sp_index, g, _, K = case
+    N, E = ptr.numel() - 1, idx.numel()
     gs = mk.spgemm_backward(ptr, idx, val, g, sp_index, N, E, K, D)
     cols = np.random.RandomState(1).choice(N, 400, replace=False)
     ix = idx.cpu().numpy()
