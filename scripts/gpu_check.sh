@@ -10,7 +10,7 @@ ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > "$OUT/gpu_tests.log" 2>&1; rc=$?
+      timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/gpu_tests.log" 2>&1; rc=$?
       tail -3 "$OUT/gpu_tests.log"; ok $rc || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?

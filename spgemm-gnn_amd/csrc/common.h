@@ -17,8 +17,12 @@ constexpr int kFwdThreads = 256;        // 4 waves
 constexpr int kBwdThreads = 512;        // 8 waves
 constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
 constexpr int kFwdUnroll = 8;           // independent sub-steps in flight per wave
-constexpr int kBwdUnroll = 16;
+constexpr int kBwdUnroll = 8;
 constexpr int kBwdTasksPerCu = 8;
+constexpr int kXcds = 8;
+constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (S = 2, 4 measured slower)
+// Records past the end of the backward edge list that a wave may read (and ignore).
+constexpr int kBwdRecPad = (kBwdThreads / kWave) * kWave * 16 + kWave;  // MI355X: 8 XCDs, work-groups dealt round-robin (speed only)
 constexpr int kBwdLdsBudget = 150 * 1024; // one 512-thread work-group per CU
 
 // Thread-local error message plumbing for maxk_last_error().
@@ -79,7 +83,8 @@ struct BwdTask {
   int32_t e0;
   int32_t e1;
   int32_t shared;
-  int32_t pad[3];
+  int32_t group;  // selector slot group (packed path): slots [group * k/S, (group+1) * k/S)
+  int32_t pad[2];
 };
 static_assert(sizeof(BwdTask) == 32, "BwdTask is 2 x dwordx4");
 
@@ -140,5 +145,11 @@ struct maxk_plan {
   int32_t* bwd_row = nullptr;    // destination row r of each reordered edge
   int32_t* bwd_col = nullptr;    // source column c
   float* bwd_val = nullptr;      // val snapshot
+  // packed backward path (k % 4 == 0, f32 CAS accumulators, grad_out < 4 GiB): one 12-B
+  // record per reordered edge {row * D * 4, column within its block, val} replaces
+  // bwd_row/bwd_col/bwd_val, and a per-call selector table in lane order
+  uint32_t* bwd_rec = nullptr;   // [num_edges + kBwdRecPad][3]
+  uint32_t* bwd_sel = nullptr;   // [S][num_cols][k / 4S] workspace: 4 selectors per lane
+  int32_t bwd_slot_groups = 1;   // S
   int64_t device_bytes = 0;
 };

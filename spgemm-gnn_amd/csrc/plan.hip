@@ -135,6 +135,43 @@ __global__ void key_offsets_kernel(const uint32_t* __restrict__ skeys, int64_t E
   offs[b] = (int32_t)lo;
 }
 
+// Backward chunk boundaries: for block b (edges [boffs[b], boffs[b+1]) sorted by row) and row
+// bound j, the first edge of the block whose row is >= rows[j].
+__global__ void chunk_offsets_kernel(const int32_t* __restrict__ erow,
+                                     const int32_t* __restrict__ boffs, int nblocks,
+                                     const int32_t* __restrict__ rows, int nb,
+                                     int32_t* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nblocks * nb) return;
+  const int b = t / nb, j = t - b * nb;
+  int64_t lo = boffs[b], hi = boffs[b + 1];
+  const int32_t r = rows[j];
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (erow[mid] < r) lo = mid + 1; else hi = mid;
+  }
+  out[t] = (int32_t)lo;
+}
+
+// Packed backward records {row * D * 4 (byte offset of the grad_out row), column within the
+// block, val}; with perm != nullptr only the val field is refreshed from the CSR order.
+__global__ void build_bwd_rec_kernel(const int32_t* __restrict__ perm,
+                                     const int32_t* __restrict__ row,
+                                     const int32_t* __restrict__ col,
+                                     const float* __restrict__ val, int64_t E, int C, int D,
+                                     uint32_t* __restrict__ rec) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid_for caps the grid
+    if (perm) {
+      rec[3 * e + 2] = __float_as_uint(val[perm[e]]);
+      continue;
+    }
+    rec[3 * e] = (uint32_t)row[e] * (uint32_t)D * 4u;
+    rec[3 * e + 1] = (uint32_t)(col[e] % C);
+    rec[3 * e + 2] = __float_as_uint(val[e]);
+  }
+}
+
 static void dfree(void* q) { if (q) (void)hipFree(q); }
 
 static int grid_for(int64_t n, int threads) {
@@ -156,6 +193,8 @@ static void free_plan(maxk_plan* p) {
   dfree(p->bwd_row);
   dfree(p->bwd_col);
   dfree(p->bwd_val);
+  dfree(p->bwd_rec);
+  dfree(p->bwd_sel);
   delete p;
 }
 
@@ -249,6 +288,11 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   MAXK_CHECK_ARG((o.fwd_unroll == 0 || o.fwd_unroll == 8 || o.fwd_unroll == 16) &&
                      (o.bwd_unroll == 0 || o.bwd_unroll == 8 || o.bwd_unroll == 16),
                  "maxk_plan_create: unroll must be 0, 8 or 16");
+  MAXK_CHECK_ARG(o.bwd_order == 0 || o.bwd_order == 1,
+                 "maxk_plan_create: bwd_order must be 0 or 1");
+  MAXK_CHECK_ARG(o.bwd_slot_groups >= 0 && o.bwd_slot_groups <= 64 &&
+                     (o.bwd_slot_groups & (o.bwd_slot_groups - 1)) == 0,
+                 "maxk_plan_create: bwd_slot_groups must be 0 or a power of two <= 64");
   p->fwd_unroll = o.fwd_unroll ? o.fwd_unroll : kFwdUnroll;
   p->bwd_unroll = o.bwd_unroll ? o.bwd_unroll : kBwdUnroll;
   {
@@ -428,9 +472,32 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     }
   }
   const int lds_budget = o.bwd_lds_bytes ? o.bwd_lds_bytes : kBwdLdsBudget;
-  int C = std::max(1, lds_budget / ((k + 1) * (int)acc_bytes(p->bwd_acc)));
+  // packed path (sspmm_bwd4_kernel): f32 accumulators, 4 selector slots per lane, grad_out
+  // addressable with 32-bit byte offsets
+  const bool packed = E > 0 && k % 4 == 0 && p->bwd_feats == 4 &&
+                      p->bwd_acc == MAXK_ACC_F32_CAS &&
+                      (uint64_t)N * (uint64_t)D * 4u <= 0xffffffffull;
+  // Slot groups: the k selector slots are split into S groups of k/S consecutive (sorted,
+  // hence clustered) slots, one work-group per (block, group). An edge then touches the
+  // few grad_out lines its group's features fall in, and a block spans S times more
+  // columns, so more edges share each fetched row (SSpMM is bound by L1-miss requests).
+  int S = 1;
+  if (packed) {
+    S = o.bwd_slot_groups ? o.bwd_slot_groups : kBwdSlotGroups;
+    while (S > 1 && (k % (4 * S)) != 0) S >>= 1;
+  }
+  p->bwd_slot_groups = S;
+  const int nslots = k / S;
+  int C = std::max(1, lds_budget / ((nslots + 1) * (int)acc_bytes(p->bwd_acc)));
   C = std::min(C, std::max(NC, 1));
-  const int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
+  const bool xcd_order = o.bwd_order == 0;
+  int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
+  if (xcd_order && nblocks >= kXcds) {
+    // a multiple of the XCD count, so every XCD owns the same number of column blocks
+    nblocks = (nblocks + kXcds - 1) / kXcds * kXcds;
+    C = (NC + nblocks - 1) / nblocks;
+    nblocks = (NC + C - 1) / C;
+  }
   p->bwd_block_cols = C;
   p->n_bwd_blocks = nblocks;
   std::vector<int64_t> offs(nblocks + 1, 0);
@@ -479,27 +546,91 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     for (int b = 0; b <= nblocks; ++b) offs[b] = offs32[b];
   }
   const int64_t target_tasks = (int64_t)(o.bwd_tasks_per_cu ? o.bwd_tasks_per_cu : kBwdTasksPerCu) * cus;
-  const int chunks = (int)std::max<int64_t>(1, (target_tasks + nblocks - 1) / std::max(nblocks, 1));
+  const int chunks = (int)std::max<int64_t>(
+      1, (target_tasks + (int64_t)nblocks * S - 1) / std::max<int64_t>((int64_t)nblocks * S, 1));
   std::vector<BwdTask> btasks;
   int nshared = 0;
-  for (int b = 0; b < nblocks; ++b) {
-    const int64_t o0 = offs[b], o1 = offs[b + 1];
-    const int64_t nnz = o1 - o0;
-    const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, nnz / 1024));
-    if (nch > 1) ++nshared;
-    for (int i = 0; i < nch; ++i) {
-      BwdTask t{};
-      t.col0 = b * C;
-      t.ncols = std::min(C, NC - t.col0);
-      t.e0 = (int32_t)(o0 + nnz * i / nch);
-      t.e1 = (int32_t)(o0 + nnz * (i + 1) / nch);
-      t.shared = nch > 1;
-      btasks.push_back(t);
+  if (xcd_order && E > 0 && nblocks > 0) {
+    // Row-chunk-major, XCD-aware order. Chunk j of every block covers the same rows
+    // [R_j, R_j+1) (equal edge counts over the whole graph), so the work-groups that run
+    // together sweep the same rows of G and share its lines in their XCD's L2. Work-groups
+    // are dealt round-robin over the 8 XCDs (blockIdx % 8 labels the work-groups sharing an
+    // XCD; speed only, correctness never depends on it): XCD x owns blocks b = x (mod 8)
+    // and walks (chunk, block) in chunk-major order.
+    const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, E / 1024 + 1));
+    std::vector<int32_t> rb(nch + 1);
+    for (int j = 0; j <= nch; ++j) {
+      const int64_t target = E * j / nch;
+      rb[j] = (int32_t)(std::lower_bound(hp.begin(), hp.end(), (int32_t)target) - hp.begin());
     }
+    rb[0] = 0;
+    rb[nch] = N;
+    int32_t *d_rb = nullptr, *d_co = nullptr;
+    std::vector<int32_t> co((size_t)nblocks * (nch + 1));
+    auto chunk_cleanup = [&]() { dfree(d_rb); dfree(d_co); };
+#define CH_TRY(x)                                        \
+    do {                                                 \
+      hipError_t e_ = (x);                               \
+      if (e_ != hipSuccess) {                            \
+        chunk_cleanup();                                 \
+        PLAN_TRY(e_);                                    \
+      }                                                  \
+    } while (0)
+    CH_TRY(hipMalloc(&d_rb, sizeof(int32_t) * (nch + 1)));
+    CH_TRY(hipMalloc(&d_co, sizeof(int32_t) * co.size()));
+    CH_TRY(hipMemcpyAsync(d_rb, rb.data(), sizeof(int32_t) * (nch + 1), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(chunk_offsets_kernel, dim3((int)((co.size() + 255) / 256)), dim3(256), 0, s,
+                       p->bwd_row, reinterpret_cast<const int32_t*>(d_offs), nblocks, d_rb,
+                       nch + 1, d_co);
+    CH_TRY(hipGetLastError());
+    CH_TRY(hipMemcpyAsync(co.data(), d_co, sizeof(int32_t) * co.size(), hipMemcpyDeviceToHost, s));
+    CH_TRY(hipStreamSynchronize(s));
+    chunk_cleanup();
+#undef CH_TRY
+    std::vector<std::vector<BwdTask>> per_xcd(kXcds);
+    for (int j = 0; j < nch; ++j) {
+      for (int b = 0; b < nblocks; ++b) {
+        for (int g = 0; g < S; ++g) {  // the groups of a block share its edge stream
+          BwdTask t{};
+          t.col0 = b * C;
+          t.ncols = std::min(C, NC - t.col0);
+          t.e0 = co[(size_t)b * (nch + 1) + j];
+          t.e1 = co[(size_t)b * (nch + 1) + j + 1];
+          t.shared = nch > 1;
+          t.group = g;
+          per_xcd[b % kXcds].push_back(t);
+        }
+      }
+    }
+    if (nch > 1) nshared = nblocks;
+    size_t len = 0;
+    for (auto& v : per_xcd) len = std::max(len, v.size());
+    btasks.assign(len * kXcds, BwdTask{});  // padding tasks have ncols == 0
+    for (int x = 0; x < kXcds; ++x)
+      for (size_t i = 0; i < per_xcd[x].size(); ++i) btasks[i * kXcds + x] = per_xcd[x][i];
+  } else {
+    for (int b = 0; b < nblocks; ++b) {
+      const int64_t o0 = offs[b], o1 = offs[b + 1];
+      const int64_t nnz = o1 - o0;
+      const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, nnz / 1024));
+      if (nch > 1) ++nshared;
+      for (int i = 0; i < nch; ++i) {
+        for (int g = 0; g < S; ++g) {
+          BwdTask t{};
+          t.col0 = b * C;
+          t.ncols = std::min(C, NC - t.col0);
+          t.e0 = (int32_t)(o0 + nnz * i / nch);
+          t.e1 = (int32_t)(o0 + nnz * (i + 1) / nch);
+          t.shared = nch > 1;
+          t.group = g;
+          btasks.push_back(t);
+        }
+      }
+    }
+    std::stable_sort(btasks.begin(), btasks.end(), [](const BwdTask& a, const BwdTask& b) {
+      return (a.e1 - a.e0) > (b.e1 - b.e0);
+    });
   }
-  std::stable_sort(btasks.begin(), btasks.end(), [](const BwdTask& a, const BwdTask& b) {
-    return (a.e1 - a.e0) > (b.e1 - b.e0);
-  });
   p->n_bwd_tasks = (int32_t)btasks.size();
   p->n_bwd_shared = nshared;
   if (!btasks.empty()) {
@@ -507,6 +638,22 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     PLAN_TRY(hipMemcpyAsync(p->bwd_tasks, btasks.data(), sizeof(BwdTask) * btasks.size(),
                             hipMemcpyHostToDevice, s));
     p->device_bytes += sizeof(BwdTask) * btasks.size();
+  }
+  // packed backward path: records instead of the three parallel arrays
+  if (packed) {
+    PLAN_TRY(hipMalloc(&p->bwd_rec, sizeof(uint32_t) * 3 * (size_t)(E + kBwdRecPad)));
+    PLAN_TRY(hipMemsetAsync(p->bwd_rec + 3 * E, 0, sizeof(uint32_t) * 3 * kBwdRecPad, s));
+    hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, nullptr,
+                       p->bwd_row, p->bwd_col, p->bwd_val, E, C, D, p->bwd_rec);
+    PLAN_TRY(hipGetLastError());
+    PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)std::max(NC, 1) * k));
+    PLAN_TRY(hipStreamSynchronize(s));
+    dfree(p->bwd_row);
+    dfree(p->bwd_col);
+    dfree(p->bwd_val);
+    p->bwd_row = p->bwd_col = nullptr;
+    p->bwd_val = nullptr;
+    p->device_bytes += (int64_t)NC * k + 12ll * kBwdRecPad;  // rec replaces row/col/val
   }
   PLAN_TRY(hipStreamSynchronize(s));
   dfree(row_of);
@@ -524,9 +671,14 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
 extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* stream) {
   MAXK_CHECK_ARG(p != nullptr, "maxk_plan_refresh_values: plan is null");
   if (p->num_edges == 0) return MAXK_OK;
-  hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
-                     (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
-                     nullptr, nullptr, p->bwd_val);
+  if (p->bwd_rec)
+    hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
+                       (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
+                       p->bwd_block_cols, p->dim_origin, p->bwd_rec);
+  else
+    hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
+                       (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
+                       nullptr, nullptr, p->bwd_val);
   if (p->fwd_perm)
     hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
                        (hipStream_t)stream, p->fwd_perm, nullptr, nullptr, val, p->num_edges,

@@ -219,6 +219,7 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
   // [c][k] layout with lane-contiguous slots put a wave on 8 banks: 8-way conflicts).
   T* bacc = reinterpret_cast<T*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
+  if (t.ncols == 0 || (t.shared && t.e0 == t.e1)) return;  // padding / nothing to add
   const int KS = k + 1;
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += kBwdThreads) bacc[i] = T(0);
@@ -319,6 +320,136 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
     const int pos = cl * KS + l;
     if (t.shared) global_add(dst + i, (float)bacc[pos]);
     else dst[i] = (float)bacc[pos];
+  }
+}
+
+
+// Packed backward (k % 4 == 0, f32 accumulators): the same (block, row)-ordered sweep as
+// sspmm_bwd_kernel<4, ...> with the per-edge work cut to the memory operations it needs:
+// one dwordx3 record load {row * D * 4, column in block, val}, one dword of four selectors
+// already in lane order (pack_sel_kernel), four buffer_load_dword gathers of grad_out with
+// 32-bit offsets, and the LDS compare-and-swap adds issued as a batch (all reads, then all
+// CAS, then a retry loop for the rare lanes whose CAS lost a race).
+__global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int n, int k, int S,
+                                uint32_t* __restrict__ sel) {
+  // sel[(g * n + c) * L + q] = slots g*k/S + q + L*i, i = 0..3, of column c (L = k / 4S)
+  const int L = k / (4 * S);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * L * S) return;
+  const int g = i / (n * L);
+  const int r = i - g * (n * L);
+  const int c = r / L, q = r - c * L;
+  const uint8_t* s = sp_index + (size_t)c * k + g * (k / S) + q;
+  sel[i] = (uint32_t)s[0] | ((uint32_t)s[L] << 8) | ((uint32_t)s[2 * L] << 16) |
+           ((uint32_t)s[3 * L] << 24);
+}
+
+template <int U>
+__global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
+    const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
+    const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
+    float* __restrict__ grad_sp, int k, int S, int ncols_all) {
+  extern __shared__ __align__(16) double bsmem[];
+  float* bacc = reinterpret_cast<float*>(bsmem);
+  const BwdTask t = tasks[blockIdx.x];
+  if (t.ncols == 0 || (t.shared && t.e0 == t.e1)) return;  // padding / nothing to add
+  const int ns = k / S;  // slots of this group: [t.group * ns, (t.group + 1) * ns)
+  const int KS = ns + 1;
+  const int nacc = t.ncols * KS;
+  for (int i = threadIdx.x; i < nacc; i += kBwdThreads) bacc[i] = 0.f;
+  __syncthreads();
+
+  const int L = ns >> 2;  // lanes per edge, 4 slots each: q, q + L, q + 2L, q + 3L
+  const int EPS = kWave / L;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int slot = lane / L;
+  const int q = lane - slot * L;
+  const bool lane_on = slot < EPS;
+  constexpr int kWaves = kBwdThreads / kWave;
+  const __amdgpu_buffer_rsrc_t gr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
+  const uint32_t* selb = sel + ((size_t)t.group * ncols_all + t.col0) * L + q;
+  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + q;
+
+  for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
+    uint32_t go[U], cl[U];
+    float v[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * EPS + slot;  // past e1: a padded or neighbouring record
+      ok[u] = lane_on && e < t.e1;
+      const uint3 r3 = *reinterpret_cast<const uint3*>(rec + 3 * (size_t)e);
+      go[u] = r3.x;
+      cl[u] = r3.y;
+      v[u] = __uint_as_float(r3.z);
+    }
+    uint32_t s[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[u] = selb[cl[u] * L];
+    float x[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t off = go[u] + (((s[u] >> (8 * i)) & 0xffu) << 2);
+        x[u][i] = v[u] * __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
+      }
+    }
+    unsigned old[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      unsigned* a = accq + cl[u] * KS;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        old[u][i] = __hip_atomic_load(a + i * L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    unsigned got[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      unsigned* a = accq + cl[u] * KS;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        got[u][i] = old[u][i];
+        if (ok[u]) {
+          unsigned expected = old[u][i];
+          __hip_atomic_compare_exchange_strong(
+              a + i * L, &expected, __float_as_uint(__uint_as_float(old[u][i]) + x[u][i]),
+              __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          got[u][i] = expected;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      unsigned* a = accq + cl[u] * KS;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (ok[u] && got[u][i] != old[u][i]) {
+          unsigned cur = got[u][i];
+          while (true) {
+            unsigned expected = cur;
+            __hip_atomic_compare_exchange_strong(
+                a + i * L, &expected, __float_as_uint(__uint_as_float(cur) + x[u][i]),
+                __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (expected == cur) break;
+            cur = expected;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  float* dst = grad_sp + (size_t)t.col0 * k + t.group * ns;
+  const int n = t.ncols * ns;
+  for (int i = threadIdx.x; i < n; i += kBwdThreads) {
+    const int c = i / ns;
+    const int l = i - c * ns;
+    const float a = bacc[c * KS + l];
+    if (t.shared) global_add(dst + (size_t)c * k + l, a);
+    else dst[(size_t)c * k + l] = a;
   }
 }
 
@@ -462,6 +593,26 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   if (plan->n_bwd_tasks == 0) return MAXK_OK;
   const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k, plan->bwd_acc);
   const dim3 grid(plan->n_bwd_tasks), block(kBwdThreads);
+  if (plan->bwd_rec) {
+    const int S = plan->bwd_slot_groups;
+    const int nsel = plan->num_cols * (k / 4);
+    hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
+                       plan->num_cols, k, S, plan->bwd_sel);
+    const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
+    const size_t lds4 = (size_t)plan->bwd_block_cols * (k / S + 1) * sizeof(float);
+#define BWD4_LAUNCH(UU)                                                                   \
+    do {                                                                                  \
+      if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU>, lds4));         \
+      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU>), grid, block, lds4, s, plan->bwd_tasks,  \
+                         plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, grad_sp, k, S,  \
+                         plan->num_cols);                                                 \
+    } while (0)
+    if (plan->bwd_unroll == 16) BWD4_LAUNCH(16);
+    else BWD4_LAUNCH(8);
+#undef BWD4_LAUNCH
+    MAXK_LAUNCH_CHECK("sspmm_bwd launch");
+    return MAXK_OK;
+  }
 #define BWD_LAUNCH1(F, A, UU)                                                             \
   do {                                                                                    \
     if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd_kernel<F, A, UU>, lds));       \

@@ -58,7 +58,9 @@ class PlanOptions(ctypes.Structure):
         ("fwd_persistent", _i32),
         ("fwd_unroll", _i32),
         ("bwd_unroll", _i32),
-        ("reserved", _i32 * 1),
+        ("bwd_order", _i32),
+        ("bwd_slot_groups", _i32),
+        ("reserved", _i32 * 3),
     ]
 
 

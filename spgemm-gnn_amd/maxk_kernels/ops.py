@@ -174,7 +174,7 @@ class GraphPlan:
 
     def __del__(self):
         h = getattr(self, "handle", None)
-        if h is not None and h.value:
+        if h is not None and h.value and lib is not None:
             lib.maxk_plan_destroy(h)
             self.handle = ctypes.c_void_p(0)
 

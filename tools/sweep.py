@@ -54,8 +54,8 @@ def main():
 
     fwd_variants = [dict()] + [dict(fwd_tile_rows=r, fwd_unroll=u)
                                for r, u in itertools.product((16, 32), (8, 16))]
-    bwd_variants = [dict()] + [dict(bwd_unroll=u, bwd_tasks_per_cu=1, bwd_lds_bytes=b)
-                               for u, b in itertools.product((8, 16), (76800, 61440, 38400, 30720, 19200))]
+    bwd_variants = [dict(bwd_features_per_lane=1)] + [
+        dict(bwd_slot_groups=s, bwd_tasks_per_cu=tp) for s, tp in itertools.product((1, 2, 4), (4, 8))]
     ref_out = ref_grad = None
     results = []
     if args.which in ("fwd", "both"):
