@@ -11,7 +11,7 @@ for f in glob.glob(os.path.join(root, "pass*", "**", "*counter_collection.csv"),
     for r in csv.DictReader(open(f)):
         name = r.get("Kernel_Name", "")
         short = ("spgemm_fwd" if "spgemm_fwd_kernel" in name else
-                 "sspmm_bwd" if "sspmm_bwd_kernel" in name else
+                 "sspmm_bwd" if "sspmm_bwd" in name else
                  "pack_cbsr" if "pack_cbsr" in name else None)
         if short is None:
             continue

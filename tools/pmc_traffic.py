@@ -15,7 +15,7 @@ import json
 import os
 from collections import defaultdict
 
-SHORT = (("spgemm_fwd_kernel", "spgemm_fwd"), ("sspmm_bwd_kernel", "sspmm_bwd"),
+SHORT = (("spgemm_fwd_kernel", "spgemm_fwd"), ("sspmm_bwd", "sspmm_bwd"),
          ("pack_cbsr", "pack_cbsr"), ("topk_exact", "topk"))
 
 
