@@ -1,0 +1,96 @@
+"""GPU: the row-partitioned path of maxk_kernels.dist on one device.
+
+* emulated W-rank partition: each rank's rectangular plan (columns remapped into the padded
+  all-gather table) run on the GPU, the all-gather / reduce-scatter done with tensor ops;
+  the union of the ranks' outputs must match the oracle on the whole graph;
+* ShardedAggregation end to end over a real RCCL ("nccl") process group of world size 1.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+import maxk_kernels as mk
+from maxk_kernels import graphs
+from maxk_kernels.dist import RowPartition, ShardedAggregation
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph(n=6000, e=150_000, seed=41):
+    p, i = graphs.synthetic_csr(n, e, seed=seed)
+    return p, i, graphs.sage_mean_values(p)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("k", [16, 32])
+def test_emulated_partition_matches_oracle(gpu, world, k):
+    p, i, v = _graph()
+    n, d = p.numel() - 1, 256
+    x = graphs.features(n, d, seed=5)
+    g = graphs.features(n, d, seed=6)
+    od, oi = oracle.maxk(x.numpy(), k)
+    ref_f, mag_f = oracle.spgemm_forward(p.numpy(), i.numpy(), v.numpy(), od, oi, d, with_mag=True)
+    ref_b, mag_b = oracle.sspmm_backward(p.numpy(), i.numpy(), v.numpy(), g.numpy(), oi,
+                                         with_mag=True)
+    ptr, idx, val = p.to(gpu), i.to(gpu), v.to(gpu)
+    part = RowPartition(ptr, world)
+    m = part.max_rows
+    # the padded all-gather table every rank would hold
+    table_d = torch.zeros((part.padded_rows, k), device=gpu)
+    table_i = torch.zeros((part.padded_rows, k), dtype=torch.uint8, device=gpu)
+    for q in range(world):
+        a, b = part.rows(q)
+        table_d[q * m: q * m + (b - a)] = torch.from_numpy(od[a:b]).to(gpu)
+        table_i[q * m: q * m + (b - a)] = torch.from_numpy(oi[a:b]).to(gpu)
+    y = torch.empty((n, d), device=gpu)
+    grad_table = torch.zeros((part.padded_rows, k), device=gpu)
+    for q in range(world):
+        a, b = part.rows(q)
+        lp, li, lv = part.local_csr(ptr, idx, val, q)
+        plan = mk.GraphPlan(lp, li, lv, b - a, li.numel(), d, k, num_cols=part.padded_rows)
+        y[a:b] = plan.forward(table_d, table_i)
+        grad_table += plan.backward(g[a:b].contiguous().to(gpu), table_i)   # reduce-scatter
+    gs = torch.cat([grad_table[q * m: q * m + (part.rows(q)[1] - part.rows(q)[0])]
+                    for q in range(world)])
+    ok, worst = oracle.close_enough(y.cpu().numpy(), ref_f, mag_f)
+    assert ok, worst
+    # per-rank partials summed in f32: bound by the summed magnitude
+    ok, worst = oracle.close_enough(gs.cpu().numpy(), ref_b, mag_b, rtol=2e-5)
+    assert ok, worst
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_sharded_aggregation_rccl_world1(gpu):
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    try:
+        p, i, v = _graph(n=4000, e=90_000, seed=42)
+        n, d, k = p.numel() - 1, 256, 16
+        ptr, idx, val = p.to(gpu), i.to(gpu), v.to(gpu)
+        x = graphs.features(n, d, seed=7).to(gpu)
+        g = graphs.features(n, d, seed=8).to(gpu)
+        sd, si = mk.maxk_forward(x, k, return_index=True)
+        part = RowPartition(ptr, 1)
+        shard = ShardedAggregation(part, 0, ptr, idx, val, d, k)
+        y = shard.forward(sd, si)
+        gs = shard.backward(g)
+        y_ref, _ = mk.spgemm_forward(ptr, idx, val, sd, si, n, idx.numel(), k, d)
+        gs_ref = mk.spgemm_backward(ptr, idx, val, g, si, n, idx.numel(), k, d)
+        torch.cuda.synchronize()
+        assert torch.allclose(y, y_ref, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(gs, gs_ref, rtol=1e-5, atol=1e-6)
+    finally:
+        dist.destroy_process_group()

@@ -259,3 +259,40 @@ def test_dense_spmm_vs_oracle(gpu):
     y = mk.dense_spmm(ptr, idx, val, x.to(gpu))
     # both sides accumulate in f32 in different orders: bound by the summed magnitude
     assert_close(y, ref, mag, rtol=2e-6 * 64)
+
+
+# ------------------------------------------------------------------------ plan options
+# every maxk_plan_options knob the C ABI exposes selects a different kernel organisation;
+# each must give the same results (the defaults are covered above)
+PLAN_OPTIONS = [
+    dict(fwd_tile_rows=16), dict(fwd_tile_rows=1), dict(fwd_accumulator="f32_cas"),
+    dict(fwd_phases=3), dict(fwd_persistent=1), dict(fwd_unroll=16), dict(fwd_task_cap=512),
+    dict(bwd_accumulator="f64"), dict(bwd_features_per_lane=1), dict(bwd_order=1),
+    dict(bwd_unroll=16), dict(bwd_slot_groups=2), dict(bwd_slot_groups=4),
+    dict(bwd_lds_bytes=4096), dict(bwd_tasks_per_cu=1), dict(bwd_tasks_per_cu=32),
+]
+
+
+@pytest.mark.parametrize("opts", PLAN_OPTIONS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+@pytest.mark.parametrize("k", [16, 32])
+def test_plan_options_vs_oracle(gpu, opts, k):
+    p, ix, v = GRAPHS["heavy_split"]()
+    n, d = p.size - 1, 256
+    x = graphs.features(n, d, seed=k)
+    g = graphs.features(n, d, seed=k + 1)
+    od, oi = oracle.maxk(x.numpy(), k)
+    ref_f, mag_f = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    ref_b, mag_b = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k, options=opts)
+    assert_close(plan.forward(to_dev(od, gpu), to_dev(oi, gpu)), ref_f, mag_f)
+    assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref_b, mag_b)
+
+
+def test_plan_options_rejected(gpu):
+    p, ix, v = GRAPHS["single_node"]()
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    for bad in (dict(fwd_unroll=7), dict(bwd_order=3), dict(bwd_slot_groups=3),
+                dict(fwd_tile_rows=33), dict(bwd_lds_bytes=1 << 20)):
+        with pytest.raises(RuntimeError):
+            mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
