@@ -19,6 +19,7 @@ constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
 constexpr int kFwdUnroll = 8;           // independent sub-steps in flight per wave
 constexpr int kBwdUnroll = 8;
 constexpr int kBwdTasksPerCu = 8;
+constexpr int kBwdMinTaskEdges = 16384;  // a chunk's flush costs ~as much as ~4k edges
 constexpr int kXcds = 8;
 constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (S = 2, 4 measured slower)
 // Records past the end of the backward edge list that a wave may read (and ignore).

@@ -265,6 +265,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: unknown accumulator kind");
   MAXK_CHECK_ARG(o.bwd_lds_bytes >= 0 && o.bwd_lds_bytes <= 160 * 1024 &&
                      o.bwd_tasks_per_cu >= 0 && o.fwd_task_cap >= 0 && o.fwd_phases >= 0 &&
+                     o.bwd_min_task_edges >= 0 &&
                      o.fwd_phases <= 64,
                  "maxk_plan_create: bad option value");
   *out_plan = nullptr;
@@ -548,6 +549,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   const int64_t target_tasks = (int64_t)(o.bwd_tasks_per_cu ? o.bwd_tasks_per_cu : kBwdTasksPerCu) * cus;
   const int chunks = (int)std::max<int64_t>(
       1, (target_tasks + (int64_t)nblocks * S - 1) / std::max<int64_t>((int64_t)nblocks * S, 1));
+  const int64_t min_task_edges = o.bwd_min_task_edges > 0 ? o.bwd_min_task_edges : kBwdMinTaskEdges;
   std::vector<BwdTask> btasks;
   int nshared = 0;
   if (xcd_order && E > 0 && nblocks > 0) {
@@ -557,7 +559,11 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     // are dealt round-robin over the 8 XCDs (blockIdx % 8 labels the work-groups sharing an
     // XCD; speed only, correctness never depends on it): XCD x owns blocks b = x (mod 8)
     // and walks (chunk, block) in chunk-major order.
-    const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, E / 1024 + 1));
+    // every chunk task flushes its whole block (C * k atomics) however few edges it has:
+    // keep >= kBwdMinTaskEdges edges per task (a row shard of a multi-GPU partition has
+    // 1/W of the edges over the same blocks)
+    const int nch = (int)std::max<int64_t>(
+        1, std::min<int64_t>(chunks, E / ((int64_t)nblocks * min_task_edges)));
     std::vector<int32_t> rb(nch + 1);
     for (int j = 0; j <= nch; ++j) {
       const int64_t target = E * j / nch;
@@ -612,7 +618,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     for (int b = 0; b < nblocks; ++b) {
       const int64_t o0 = offs[b], o1 = offs[b + 1];
       const int64_t nnz = o1 - o0;
-      const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, nnz / 1024));
+      const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, nnz / min_task_edges));
       if (nch > 1) ++nshared;
       for (int i = 0; i < nch; ++i) {
         for (int g = 0; g < S; ++g) {

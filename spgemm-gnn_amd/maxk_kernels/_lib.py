@@ -60,7 +60,8 @@ class PlanOptions(ctypes.Structure):
         ("bwd_unroll", _i32),
         ("bwd_order", _i32),
         ("bwd_slot_groups", _i32),
-        ("reserved", _i32 * 3),
+        ("bwd_min_task_edges", _i32),
+        ("reserved", _i32 * 2),
     ]
 
 
