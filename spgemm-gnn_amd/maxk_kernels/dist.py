@@ -7,8 +7,8 @@ exchange per direction:
 * partition: contiguous row ranges balanced by nnz; rank q owns rows [start_q, end_q),
   their CSR slice (columns keep pointing at any node) and computes the top-k of its own
   rows (weights are replicated);
-* forward : RCCL all-gather of the k-sparse CBSR block (sp_data f32 + sp_index u8, 5k
-  bytes per node) into a table padded to W x max_rows rows, then the local SpGEMM over
+* forward : one RCCL all-gather of the k-sparse CBSR block (sp_data f32 + sp_index u8 as
+  5k bytes per node) into a table padded to W x max_rows rows, then the local SpGEMM over
   the rank's rows with a rectangular plan whose column ids are remapped into that
   padded table (remapping is done once, at partition time);
 * backward: the local SSpMM produces a partial grad_sp for every (padded) column; an
@@ -88,8 +88,10 @@ class ShardedAggregation:
         self.ptr, self.idx, self.val = part.local_csr(ptr, idx, val, rank)
         dev = self.ptr.device
         m, k = part.max_rows, self.dim_k
-        self.send_data = torch.zeros((m, k), dtype=torch.float32, device=dev)
-        self.send_index = torch.zeros((m, k), dtype=torch.uint8, device=dev)
+        # one collective per step: each CBSR row travels as 5k bytes {k f32 values, k u8
+        # selectors}, split into the two tables after the all-gather
+        self.send = torch.zeros((m, 5 * k), dtype=torch.uint8, device=dev)
+        self.table_bytes = torch.empty((part.padded_rows, 5 * k), dtype=torch.uint8, device=dev)
         self.table_data = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
         self.table_index = torch.empty((part.padded_rows, k), dtype=torch.uint8, device=dev)
         self.grad_local = torch.empty((m, k), dtype=torch.float32, device=dev)
@@ -103,11 +105,12 @@ class ShardedAggregation:
 
     def gather(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> None:
         """All-gather this rank's CBSR rows into the padded table (RCCL over xGMI)."""
-        n = self.n_local
-        self.send_data[:n].copy_(sp_data_local)
-        self.send_index[:n].copy_(sp_index_local)
-        dist.all_gather_into_tensor(self.table_data, self.send_data, group=self.group)
-        dist.all_gather_into_tensor(self.table_index, self.send_index, group=self.group)
+        n, k = self.n_local, self.dim_k
+        self.send[:n, :4 * k].copy_(sp_data_local.contiguous().view(torch.uint8))
+        self.send[:n, 4 * k:].copy_(sp_index_local)
+        dist.all_gather_into_tensor(self.table_bytes, self.send, group=self.group)
+        self.table_data.view(torch.uint8).view(-1, 4 * k).copy_(self.table_bytes[:, :4 * k])
+        self.table_index.copy_(self.table_bytes[:, 4 * k:])
 
     def forward(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> torch.Tensor:
         self.gather(sp_data_local, sp_index_local)
