@@ -287,8 +287,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   p->src_idx = idx;
   p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
   MAXK_CHECK_ARG((o.fwd_unroll == 0 || o.fwd_unroll == 8 || o.fwd_unroll == 16) &&
-                     (o.bwd_unroll == 0 || o.bwd_unroll == 8 || o.bwd_unroll == 16),
-                 "maxk_plan_create: unroll must be 0, 8 or 16");
+                     (o.bwd_unroll == 0 || o.bwd_unroll == 4 || o.bwd_unroll == 8 ||
+                      o.bwd_unroll == 12 || o.bwd_unroll == 16),
+                 "maxk_plan_create: unroll must be 0, 8 or 16 (backward also 4 or 12)");
   MAXK_CHECK_ARG(o.bwd_order == 0 || o.bwd_order == 1,
                  "maxk_plan_create: bwd_order must be 0 or 1");
   MAXK_CHECK_ARG(o.bwd_slot_groups >= 0 && o.bwd_slot_groups <= 64 &&

@@ -608,6 +608,8 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
                          plan->num_cols);                                                 \
     } while (0)
     if (plan->bwd_unroll == 16) BWD4_LAUNCH(16);
+    else if (plan->bwd_unroll == 12) BWD4_LAUNCH(12);
+    else if (plan->bwd_unroll == 4) BWD4_LAUNCH(4);
     else BWD4_LAUNCH(8);
 #undef BWD4_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd launch");
@@ -622,7 +624,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   } while (0)
 #define BWD_LAUNCH(F, A)                                                                  \
   do {                                                                                    \
-    if (plan->bwd_unroll == 16) BWD_LAUNCH1(F, A, 16);                                    \
+    if (plan->bwd_unroll >= 12) BWD_LAUNCH1(F, A, 16);                                    \
     else BWD_LAUNCH1(F, A, 8);                                                            \
   } while (0)
   if (plan->bwd_feats == 4) {

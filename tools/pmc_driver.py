@@ -1,5 +1,6 @@
 """Small fixed workload for rocprofv3 --pmc passes (tooling): the BASELINE config (Reddit,
 D=256, k=16), 3 SpGEMM forwards + 3 SSpMM backwards with the default plan."""
+import json
 import os
 import sys
 
@@ -20,7 +21,9 @@ e = idx.numel()
 h = graphs.features(n, 256, seed=97, device=dev)
 g = graphs.features(n, 256, seed=98, device=dev)
 sp_data, sp_index = mk.maxk_forward(h, k, return_index=True)
-plan = mk.get_plan(ptr, idx, val, n, e, 256, k)
+opts = json.loads(os.environ.get("PMC_OPTS", "{}"))
+plan = mk.GraphPlan(ptr, idx, val, n, e, 256, k, options=opts) if opts else mk.get_plan(
+    ptr, idx, val, n, e, 256, k)
 out = plan.forward(sp_data, sp_index)
 grad = plan.backward(g, sp_index)
 for _ in range(3):
