@@ -152,5 +152,6 @@ struct maxk_plan {
   uint32_t* bwd_rec = nullptr;   // [num_edges + kBwdRecPad][3]
   uint32_t* bwd_sel = nullptr;   // [S][num_cols][k / 4S] workspace: 4 selectors per lane
   int32_t bwd_slot_groups = 1;   // S
+  int32_t bwd_ks = 0;            // accumulator floats per column (k/S + 1, or k/S unpadded)
   int64_t device_bytes = 0;
 };

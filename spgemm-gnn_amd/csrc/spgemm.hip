@@ -348,13 +348,12 @@ template <int U>
 __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
-    float* __restrict__ grad_sp, int k, int S, int ncols_all) {
+    float* __restrict__ grad_sp, int k, int S, int ncols_all, int KS) {
   extern __shared__ __align__(16) double bsmem[];
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
   if (t.ncols == 0 || (t.shared && t.e0 == t.e1)) return;  // padding / nothing to add
   const int ns = k / S;  // slots of this group: [t.group * ns, (t.group + 1) * ns)
-  const int KS = ns + 1;
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += kBwdThreads) bacc[i] = 0.f;
   __syncthreads();
@@ -599,13 +598,13 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
                        plan->num_cols, k, S, plan->bwd_sel);
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
-    const size_t lds4 = (size_t)plan->bwd_block_cols * (k / S + 1) * sizeof(float);
+    const size_t lds4 = (size_t)plan->bwd_block_cols * plan->bwd_ks * sizeof(float);
 #define BWD4_LAUNCH(UU)                                                                   \
     do {                                                                                  \
       if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU>, lds4));         \
       hipLaunchKernelGGL((sspmm_bwd4_kernel<UU>), grid, block, lds4, s, plan->bwd_tasks,  \
                          plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, grad_sp, k, S,  \
-                         plan->num_cols);                                                 \
+                         plan->num_cols, plan->bwd_ks);                                   \
     } while (0)
     if (plan->bwd_unroll == 16) BWD4_LAUNCH(16);
     else if (plan->bwd_unroll == 12) BWD4_LAUNCH(12);

@@ -61,7 +61,8 @@ class PlanOptions(ctypes.Structure):
         ("bwd_order", _i32),
         ("bwd_slot_groups", _i32),
         ("bwd_min_task_edges", _i32),
-        ("reserved", _i32 * 2),
+        ("bwd_acc_pad", _i32),
+        ("reserved", _i32 * 1),
     ]
 
 
