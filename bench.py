@@ -32,6 +32,9 @@ from maxk_kernels import graphs  # noqa: E402
 from maxk_kernels.dist import RowPartition, ShardedAggregation  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+# L1-miss line-request ceiling: ~1 request of 128 B per ns per CU for L2-resident gathers
+# (tools/ubench_tcp.hip, profiles/r01/ubench_tcp.log), x 256 CUs
+L2_REQUEST_CEILING_GBS = 256 * 128.0
 
 
 def fwd_bytes(n, e, k, d):
@@ -230,11 +233,13 @@ def main():
     dom = "sspmm_bwd" if bwd_ms >= fwd_ms else "spgemm_fwd"
     achieved = bwd_gbs if dom == "sspmm_bwd" else fwd_gbs
     traffic = None
+    detail = {}
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             key = f"{args.dataset}:k{k}:d{d}:n{world}"
             traffic = tj.get(key, {}).get(dom)
+            detail = tj.get(key, {}).get(dom + "_detail", {})
         except (OSError, ValueError):
             traffic = None
 
@@ -272,6 +277,16 @@ def main():
         },
         "fwd_ms": fwd_ms,
         "bwd_ms": bwd_ms,
+        # supplementary: the bound that binds an irregular gather on gfx950 is the L1-miss
+        # line-request rate, not HBM bytes; from profiles/ PMC counters
+        "l1_request_roofline": None if "l1_miss_requests" not in detail else {
+            "kernel": dom,
+            "requests_per_launch": detail["l1_miss_requests"],
+            "achieved": detail["l1_miss_requests"] * 128 / ((bwd_ms if dom == "sspmm_bwd" else fwd_ms) * 1e-3) / 1e9,
+            "peak": L2_REQUEST_CEILING_GBS, "unit": "GB/s",
+            "frac": detail["l1_miss_requests"] * 128 / ((bwd_ms if dom == "sspmm_bwd" else fwd_ms) * 1e-3) / 1e9 / L2_REQUEST_CEILING_GBS,
+            "l2_hit_rate": detail.get("l2_hit_rate"),
+        },
         "fwd_edges_per_s": e_loc / (fwd_ms * 1e-3),
         "bwd_edges_per_s": e_loc / (bwd_ms * 1e-3),
         "fwd_roofline_frac": fwd_gbs / HBM_PEAK_GBS,

@@ -47,6 +47,12 @@ def main():
         entry[kern] = fetch + write
         entry[kern + "_detail"] = {"fetch_bytes_x2": fetch, "write_bytes": write,
                                    "dispatches": len(cs["FETCH_SIZE"])}
+        if "TCP_TCC_READ_REQ_sum" in cs:  # L1-miss line requests (128 B) per launch
+            r = cs["TCP_TCC_READ_REQ_sum"]
+            entry[kern + "_detail"]["l1_miss_requests"] = sum(r) / len(r)
+        if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs:
+            h, m = sum(cs["TCC_HIT_sum"]), sum(cs["TCC_MISS_sum"])
+            entry[kern + "_detail"]["l2_hit_rate"] = h / max(h + m, 1.0)
     doc = json.load(open(args.out)) if os.path.exists(args.out) else {}
     doc[args.key] = entry
     json.dump(doc, open(args.out, "w"), indent=1, sort_keys=True)
