@@ -302,3 +302,17 @@ def test_plan_options_rejected(gpu):
                 dict(fwd_tile_rows=33), dict(bwd_lds_bytes=1 << 20)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
+
+
+# ------------------------------------------------------------------------ rocSPARSE comparator
+def test_rocsparse_comparator_vs_oracle(gpu):
+    from maxk_kernels import baselines
+    p, ix, v = GRAPHS["synthetic"]()
+    n = p.size - 1
+    x = graphs.features(n, 64, seed=4)
+    ref = oracle.dense_spmm(p, ix, v, x.numpy())
+    mag = oracle.dense_spmm(p, ix, np.abs(v), np.abs(x.numpy()))
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    y, ms = baselines.spmm_rocsparse(ptr, idx, val, x.to(gpu), times=2)
+    assert ms > 0
+    assert_close(y, ref, mag, rtol=2e-6 * 64)
