@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <rocsparse/rocsparse.h>
 
+#include "maxk_baseline.h"
+
 #include <cstdint>
 #include <string>
 

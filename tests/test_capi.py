@@ -108,3 +108,18 @@ def test_python_checks_mirror_reference_messages():
     x = torch.zeros(4, 8)
     with pytest.raises(RuntimeError, match="input must be a CUDA tensor"):
         maxk_kernels.maxk_forward(x, 2)
+
+
+def test_baseline_library_exports_its_header():
+    header = os.path.join(ROOT, "include", "maxk_baseline.h")
+    text = re.sub(r"/\*.*?\*/", "", open(header).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(maxk_\w+)\s*\(", text)))
+    assert names == ["maxk_baseline_last_error", "maxk_spmm_rocsparse"]
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(_lib.LIB_PATH), "libmaxk_baseline.so"))
+    for n in names:
+        assert hasattr(lib, n), n
+    from maxk_kernels import baselines
+    bl = baselines._lib()
+    ms = ctypes.c_float()
+    assert bl.maxk_spmm_rocsparse(None, None, None, None, None, -1, 0, 8, 0, 0,
+                                  ctypes.byref(ms), None) == -1
