@@ -65,6 +65,30 @@ def event_time_ms(fn, reps):
     return s.elapsed_time(e) / reps
 
 
+def launch_percentiles_ms(fn, reps):
+    """Per-launch device times (one event pair around each launch): p10 / median / p90."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for s, e in evs:
+        s.record()
+        fn()
+        e.record()
+    evs[-1][1].synchronize()
+    t = sorted(s.elapsed_time(e) for s, e in evs)
+    pick = lambda q: t[min(len(t) - 1, int(round(q * (len(t) - 1))))]  # noqa: E731
+    return {"p10": pick(0.1), "median": pick(0.5), "p90": pick(0.9)}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d, sample_frac, reps, log_fn):
     """DGL-semantics dense CSR SpMM on the host cores (oracle C/OpenMP restatement of
     update_all(copy_u, sum) with edge weights; the dense MaxK output as DGL sees it),
@@ -109,6 +133,8 @@ def cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d, sample_frac, reps, log_
         "value": reps * (e_f + e_b) / (tf + tb),
         "unit": "edges/s",
         "cores": oracle.num_threads(),
+        "cpu_model": cpu_model(),
+        "host_cpus": os.cpu_count(),
         "kind": "port",
         "sample": (f"DGL-semantics dense CSR SpMM (oracle C/OpenMP, f32): forward A@X over "
                    f"rows [0,{r_f}) = {e_f} edges and backward A^T@G over rows [0,{r_b}) of "
@@ -224,6 +250,8 @@ def main():
     reps = max(5, args.steps)
     fwd_ms = event_time_ms(fwd, reps)
     bwd_ms = event_time_ms(bwd, reps)
+    fwd_pct = launch_percentiles_ms(fwd, reps)
+    bwd_pct = launch_percentiles_ms(bwd, reps)
     e_loc = info["num_edges"]
     n_loc = info["num_nodes"]
     fb = fwd_bytes(n_loc, e_loc, k, d)
@@ -277,6 +305,8 @@ def main():
         },
         "fwd_ms": fwd_ms,
         "bwd_ms": bwd_ms,
+        "fwd_launch_ms": fwd_pct,
+        "bwd_launch_ms": bwd_pct,
         # supplementary: the bound that binds an irregular gather on gfx950 is the L1-miss
         # line-request rate, not HBM bytes; from profiles/ PMC counters
         "l1_request_roofline": None if "l1_miss_requests" not in detail else {
