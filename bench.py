@@ -252,6 +252,8 @@ def main():
     bwd_ms = event_time_ms(bwd, reps)
     fwd_pct = launch_percentiles_ms(fwd, reps)
     bwd_pct = launch_percentiles_ms(bwd, reps)
+    # the MaxK producer of the path (exact top-k -> CBSR), this rank's rows
+    topk_ms = event_time_ms(lambda: mk.maxk_forward(h, k, return_index=True), reps)
     e_loc = info["num_edges"]
     n_loc = info["num_nodes"]
     fb = fwd_bytes(n_loc, e_loc, k, d)
@@ -305,6 +307,8 @@ def main():
         },
         "fwd_ms": fwd_ms,
         "bwd_ms": bwd_ms,
+        "topk_ms": topk_ms,
+        "topk_GBps": (h.numel() * 4 + 5 * h.shape[0] * k) / (topk_ms * 1e-3) / 1e9,
         "fwd_launch_ms": fwd_pct,
         "bwd_launch_ms": bwd_pct,
         # supplementary: the bound that binds an irregular gather on gfx950 is the L1-miss
