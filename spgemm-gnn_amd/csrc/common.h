@@ -12,7 +12,10 @@ namespace maxk {
 
 constexpr int kWave = 64;               // CDNA wavefront width (never 32)
 constexpr int kFwdTileRows = 32;        // default destination rows per forward work-group
-constexpr int kFwdMaxTileRows = 32;
+constexpr int kFwdMaxTileRows = 64;
+// forward edge word: source column in the low kFwdColBits bits, row within the tile above
+constexpr int kFwdColBits = 26;
+constexpr uint32_t kFwdColMask = (1u << kFwdColBits) - 1;
 constexpr int kFwdThreads = 256;        // 4 waves
 constexpr int kBwdThreads = 512;        // 8 waves
 constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
@@ -129,7 +132,7 @@ struct maxk_plan {
   int32_t bwd_unroll = 8;
   int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per phase
   int32_t* fwd_perm = nullptr;   // CSR edge id of each permuted forward edge
-  uint32_t* fwd_cr = nullptr;    // column | (row within the task << 27)
+  uint32_t* fwd_cr = nullptr;    // column | (row within the task << kFwdColBits)
   float* fwd_val = nullptr;      // val snapshot in the permuted order
   int32_t n_fwd_tasks = 0;
   int32_t* zero_rows = nullptr;  // rows written by split tasks (atomic), zeroed first

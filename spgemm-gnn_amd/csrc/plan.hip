@@ -72,7 +72,7 @@ __global__ void fwd_phase_kernel(const FwdTask* __restrict__ tasks, int ntasks,
   if (b == 0) { off[i] = lo; return; }
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if ((cr[mid] & ((1u << 27) - 1)) < bound) lo = mid + 1; else hi = mid;
+    if ((cr[mid] & kFwdColMask) < bound) lo = mid + 1; else hi = mid;
   }
   off[i] = lo;
 }
@@ -85,7 +85,7 @@ __global__ void gather_fwd_kernel(const int32_t* __restrict__ perm,
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < E;
        j += (int64_t)gridDim.x * blockDim.x) {
     const int32_t e = perm[j];
-    if (cr) cr[j] = (uint32_t)idx[e] | ((uint32_t)rl_of[e] << 27);
+    if (cr) cr[j] = (uint32_t)idx[e] | ((uint32_t)rl_of[e] << kFwdColBits);
     fval[j] = val ? val[e] : 1.0f;
   }
 }
@@ -270,6 +270,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: bad option value");
   *out_plan = nullptr;
   MAXK_CHECK_ARG(NC >= 0 && (E == 0 || NC > 0), "maxk_plan_create: num_cols out of range");
+  if ((uint32_t)NC > kFwdColMask + 1u) {
+    set_error("maxk_plan_create: more than 2^26 source columns is not supported");
+    return MAXK_ERR_UNSUPPORTED;
+  }
   MAXK_CHECK_ARG(N >= 0 && E >= 0 && E < (int64_t)INT32_MAX,
                  "maxk_plan_create: sizes out of range (E must fit int32)");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_plan_create: dim_origin must be in [1, 256]");

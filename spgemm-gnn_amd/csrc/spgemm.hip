@@ -121,7 +121,6 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   const int l0 = (lane - slot * L) * VEC;
   const bool lane_on = slot < EPS;
   constexpr int kWaves = kFwdThreads / kWave;
-  constexpr uint32_t kColMask = (1u << 27) - 1;
 
   if constexpr (VEC == 4) {
     // U sub-steps per iteration with every load issued before the first LDS update: the
@@ -145,14 +144,14 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
       uint32_t sel[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint8_t* rp = rec + (size_t)(cw[u] & kColMask) * rec_bytes;
+        const uint8_t* rp = rec + (size_t)(cw[u] & kFwdColMask) * rec_bytes;
         x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
         sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (ok[u]) {
-          T* arow = acc + (cw[u] >> 27) * D;
+          T* arow = acc + (cw[u] >> kFwdColBits) * D;
           const uint32_t sv = sel[u];
           A::add(arow + (sv & 0xffu), v[u] * x[u].x);
           A::add(arow + ((sv >> 8) & 0xffu), v[u] * x[u].y);
@@ -167,8 +166,8 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
       if (lane_on && e < t.e1) {
         const uint32_t cwv = cr[e];
         const float v = fval[e];
-        T* arow = acc + (cwv >> 27) * D;
-        const size_t rb = (size_t)(cwv & kColMask) * k;
+        T* arow = acc + (cwv >> kFwdColBits) * D;
+        const size_t rb = (size_t)(cwv & kFwdColMask) * k;
         for (int l = l0; l < k; l += L) A::add(arow + sp_index[rb + l], v * sp_data[rb + l]);
       }
     }

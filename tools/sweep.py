@@ -52,8 +52,10 @@ def main():
     sp_data, sp_index = mk.maxk_forward(h, args.k, return_index=True)
     del h
 
-    fwd_variants = [dict()] + [dict(fwd_tile_rows=r, fwd_unroll=u)
-                               for r, u in itertools.product((16, 32), (8, 16))]
+    fwd_variants = [dict(), dict(fwd_accumulator="f32_cas"),
+                    dict(fwd_tile_rows=48, fwd_accumulator="f32_cas"),
+                    dict(fwd_tile_rows=64, fwd_accumulator="f32_cas"),
+                    dict(fwd_tile_rows=64), dict(fwd_tile_rows=64, fwd_unroll=16)]
     bwd_variants = [dict(bwd_features_per_lane=1)] + [
         dict(bwd_slot_groups=s, bwd_tasks_per_cu=tp) for s, tp in itertools.product((1, 2, 4), (4, 8))]
     ref_out = ref_grad = None
