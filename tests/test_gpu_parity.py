@@ -265,7 +265,8 @@ def test_dense_spmm_vs_oracle(gpu):
 # every maxk_plan_options knob the C ABI exposes selects a different kernel organisation;
 # each must give the same results (the defaults are covered above)
 PLAN_OPTIONS = [
-    dict(fwd_tile_rows=16), dict(fwd_tile_rows=1), dict(fwd_accumulator="f32_cas"),
+    dict(fwd_tile_rows=16), dict(fwd_tile_rows=1), dict(fwd_tile_rows=64),
+    dict(fwd_accumulator="f32_cas"), dict(fwd_tile_rows=64, fwd_accumulator="f32_cas"),
     dict(fwd_phases=3), dict(fwd_persistent=1), dict(fwd_unroll=16), dict(fwd_task_cap=512),
     dict(bwd_accumulator="f64"), dict(bwd_features_per_lane=1), dict(bwd_order=1),
     dict(bwd_unroll=16), dict(bwd_slot_groups=2), dict(bwd_slot_groups=4),
@@ -299,7 +300,7 @@ def test_plan_options_rejected(gpu):
     p, ix, v = GRAPHS["single_node"]()
     ptr, idx, val = graph_on(gpu, p, ix, v)
     for bad in (dict(fwd_unroll=7), dict(bwd_order=3), dict(bwd_slot_groups=3),
-                dict(fwd_tile_rows=33), dict(bwd_lds_bytes=1 << 20)):
+                dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 
