@@ -156,5 +156,6 @@ struct maxk_plan {
   uint32_t* bwd_sel = nullptr;   // [S][num_cols][k / 4S] workspace: 4 selectors per lane
   int32_t bwd_slot_groups = 1;   // S
   int32_t bwd_ks = 0;            // accumulator floats per column (k/S + 1, or k/S unpadded)
+  int32_t bwd_sel_lds = 0;       // selector words of the block staged in LDS
   int64_t device_bytes = 0;
 };

@@ -294,6 +294,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                      (o.bwd_unroll == 0 || o.bwd_unroll == 4 || o.bwd_unroll == 8 ||
                       o.bwd_unroll == 12 || o.bwd_unroll == 16),
                  "maxk_plan_create: unroll must be 0, 8 or 16 (backward also 4 or 12)");
+  MAXK_CHECK_ARG(o.bwd_sel_lds >= 0 && o.bwd_sel_lds <= 2,
+                 "maxk_plan_create: bwd_sel_lds must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_acc_pad >= 0 && o.bwd_acc_pad <= 2,
                  "maxk_plan_create: bwd_acc_pad must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_order == 0 || o.bwd_order == 1,
@@ -498,7 +500,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   const int nslots = k / S;
   // accumulator row stride: nslots + 1 (odd: columns start on different banks) or nslots
   p->bwd_ks = nslots + ((packed && o.bwd_acc_pad == 2) ? 0 : 1);
-  int C = std::max(1, lds_budget / (p->bwd_ks * (int)acc_bytes(p->bwd_acc)));
+  p->bwd_sel_lds = packed && o.bwd_sel_lds != 2 ? 1 : 0;
+  // bytes of LDS per column: accumulators (+ staged selector bytes, nslots per column)
+  const int col_bytes = p->bwd_ks * (int)acc_bytes(p->bwd_acc) + (p->bwd_sel_lds ? nslots : 0);
+  int C = std::max(1, (lds_budget - 16) / col_bytes);
   C = std::min(C, std::max(NC, 1));
   const bool xcd_order = o.bwd_order == 0;
   int nblocks = NC > 0 ? (NC + C - 1) / C : 0;

@@ -347,17 +347,24 @@ template <int U>
 __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
-    float* __restrict__ grad_sp, int k, int S, int ncols_all, int KS) {
+    float* __restrict__ grad_sp, int k, int S, int ncols_all, int KS, int sel_lds) {
   extern __shared__ __align__(16) double bsmem[];
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
   if (t.ncols == 0 || (t.shared && t.e0 == t.e1)) return;  // padding / nothing to add
   const int ns = k / S;  // slots of this group: [t.group * ns, (t.group + 1) * ns)
+  const int L = ns >> 2;  // lanes per edge, 4 slots each: q, q + L, q + 2L, q + 3L
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += kBwdThreads) bacc[i] = 0.f;
+  // sel_lds: the block's selector words are staged in LDS behind the accumulator, so the
+  // per-edge selector lookup is an LDS read instead of an L1 miss (the G rows evict the
+  // block's 16 B/column table from the 32 KB L1)
+  const uint32_t* selg = sel + ((size_t)t.group * ncols_all + t.col0) * L;
+  uint32_t* sell = reinterpret_cast<uint32_t*>(bacc) + ((nacc + 3) & ~3);
+  if (sel_lds)
+    for (int i = threadIdx.x; i < t.ncols * L; i += kBwdThreads) sell[i] = selg[i];
   __syncthreads();
 
-  const int L = ns >> 2;  // lanes per edge, 4 slots each: q, q + L, q + 2L, q + 3L
   const int EPS = kWave / L;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
@@ -367,7 +374,7 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
   constexpr int kWaves = kBwdThreads / kWave;
   const __amdgpu_buffer_rsrc_t gr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
-  const uint32_t* selb = sel + ((size_t)t.group * ncols_all + t.col0) * L + q;
+  const uint32_t* selb = (sel_lds ? sell : selg) + q;
   unsigned* accq = reinterpret_cast<unsigned*>(bacc) + q;
 
   for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
@@ -597,13 +604,14 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
                        plan->num_cols, k, S, plan->bwd_sel);
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
-    const size_t lds4 = (size_t)plan->bwd_block_cols * plan->bwd_ks * sizeof(float);
+    const size_t lds4 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
+                        (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
 #define BWD4_LAUNCH(UU)                                                                   \
     do {                                                                                  \
       if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU>, lds4));         \
       hipLaunchKernelGGL((sspmm_bwd4_kernel<UU>), grid, block, lds4, s, plan->bwd_tasks,  \
                          plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, grad_sp, k, S,  \
-                         plan->num_cols, plan->bwd_ks);                                   \
+                         plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds);                \
     } while (0)
     if (plan->bwd_unroll == 16) BWD4_LAUNCH(16);
     else if (plan->bwd_unroll == 12) BWD4_LAUNCH(12);

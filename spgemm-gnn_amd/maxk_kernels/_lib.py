@@ -62,7 +62,7 @@ class PlanOptions(ctypes.Structure):
         ("bwd_slot_groups", _i32),
         ("bwd_min_task_edges", _i32),
         ("bwd_acc_pad", _i32),
-        ("reserved", _i32 * 1),
+        ("bwd_sel_lds", _i32),
     ]
 
 

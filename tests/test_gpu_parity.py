@@ -270,7 +270,7 @@ PLAN_OPTIONS = [
     dict(fwd_phases=3), dict(fwd_persistent=1), dict(fwd_unroll=16), dict(fwd_task_cap=512),
     dict(bwd_accumulator="f64"), dict(bwd_features_per_lane=1), dict(bwd_order=1),
     dict(bwd_unroll=16), dict(bwd_slot_groups=2), dict(bwd_slot_groups=4),
-    dict(bwd_lds_bytes=4096), dict(bwd_tasks_per_cu=1), dict(bwd_acc_pad=2),
+    dict(bwd_lds_bytes=4096), dict(bwd_tasks_per_cu=1), dict(bwd_acc_pad=2), dict(bwd_sel_lds=2),
     dict(bwd_unroll=4), dict(bwd_unroll=12),
     # chunked blocks (atomic flush into a memset grad_sp), both task orders
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256),
