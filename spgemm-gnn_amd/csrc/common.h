@@ -24,6 +24,8 @@ constexpr int kBwdUnroll = 8;
 constexpr int kBwdTasksPerCu = 8;
 constexpr int kBwdMinTaskEdges = 16384;  // a chunk's flush costs ~as much as ~4k edges
 constexpr int kXcds = 8;
+constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
+constexpr double kFwdSlotEdgeRate = 1.5e8;  // edges/s one forward work-group slot sustains
 constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (S = 2, 4 measured slower)
 // Records past the end of the backward edge list that a wave may read (and ignore).
 constexpr int kBwdRecPad = (kBwdThreads / kWave) * kWave * 16 + kWave;  // MI355X: 8 XCDs, work-groups dealt round-robin (speed only)
@@ -128,6 +130,7 @@ struct maxk_plan {
   maxk::FwdTask* fwd_tasks = nullptr;   // e0/e1 index the permuted edge order below
   int32_t fwd_phases = 1;        // column phases per forward call
   int32_t fwd_persistent = 0;    // grid = resident capacity (1) or one work-group per task
+  int32_t fwd_rot_ticks = 0;     // > 0: rotated sweeps, s_memrealtime ticks per window
   int32_t fwd_unroll = 8;        // independent sub-steps per wave (8 or 16)
   int32_t bwd_unroll = 8;
   int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per phase

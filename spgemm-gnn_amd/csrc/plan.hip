@@ -294,6 +294,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                      (o.bwd_unroll == 0 || o.bwd_unroll == 4 || o.bwd_unroll == 8 ||
                       o.bwd_unroll == 12 || o.bwd_unroll == 16),
                  "maxk_plan_create: unroll must be 0, 8 or 16 (backward also 4 or 12)");
+  MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 2,
+                 "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_sel_lds >= 0 && o.bwd_sel_lds <= 2,
                  "maxk_plan_create: bwd_sel_lds must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_acc_pad >= 0 && o.bwd_acc_pad <= 2,
@@ -443,10 +445,20 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     PLAN_TRY(hipMemcpyAsync(p->fwd_tasks, ftasks.data(), sizeof(FwdTask) * ftasks.size(),
                             hipMemcpyHostToDevice, s));
     p->device_bytes += sizeof(FwdTask) * ftasks.size();
-    // column phases: enough that one phase's slice of the packed CBSR table is ~L2-sized
+    // Column windows. Default: one launch whose tiles start their column-sorted sweep at the
+    // window a shared clock points to (fwd_rot_ticks per window, about one tile's duration
+    // per full turn), so the tiles running together on an XCD gather from nearby columns
+    // (L2 reuse). fwd_phases > 1 instead runs the windows as separate launches.
     int B = o.fwd_phases;
-    if (B == 0) B = 1;
     p->fwd_persistent = o.fwd_persistent ? 1 : 0;
+    p->fwd_rot_ticks = 0;
+    if (B <= 1 && o.fwd_rotate != 2 && k % 4 == 0 && nt > 0) {
+      B = kFwdRotWindows;
+      const double tile_edges = (double)E / nt;
+      const double tile_ticks = tile_edges / kFwdSlotEdgeRate * 1e8;  // s_memrealtime: 100 MHz
+      p->fwd_rot_ticks = (int)std::max(1.0, tile_ticks / B);
+    }
+    if (B == 0) B = 1;
     B = std::max(1, std::min(B, std::max(NC, 1)));
     p->fwd_phases = B;
     PLAN_TRY(hipMalloc(&p->fwd_phase_off, sizeof(int32_t) * nt * (B + 1)));

@@ -77,6 +77,54 @@ __global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
   }
 }
 
+// One wave's share of the forward edges [e0, e1) (VEC = 4 lanes path): U sub-steps per
+// iteration with every load issued before the first LDS update. The chain (col, val) ->
+// CBSR record -> LDS has two dependent global round trips, so memory-level parallelism
+// comes from U independent sub-steps per wave. Out-of-range lanes load a clamped (valid)
+// edge and skip the update.
+template <int U, class A>
+__device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, int wave,
+                                           int nwaves, int EPS, int slot, int l0, bool lane_on,
+                                           const uint32_t* __restrict__ cr,
+                                           const float* __restrict__ fval,
+                                           const uint8_t* __restrict__ rec, int rec_bytes,
+                                           int D, int k) {
+  using T = typename A::T;
+  const int last = e1 - 1;
+  for (int base = e0 + wave * EPS * U; base < e1; base += nwaves * EPS * U) {
+    uint32_t cw[U];
+    float v[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * EPS + slot;
+      ok[u] = lane_on && e < e1;
+      const int ec = ok[u] ? e : last;
+      cw[u] = cr[ec];
+      v[u] = fval[ec];
+    }
+    float4 x[U];
+    uint32_t sel[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint8_t* rp = rec + (size_t)(cw[u] & kFwdColMask) * rec_bytes;
+      x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
+      sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ok[u]) {
+        T* arow = acc + (cw[u] >> kFwdColBits) * D;
+        const uint32_t sv = sel[u];
+        A::add(arow + (sv & 0xffu), v[u] * x[u].x);
+        A::add(arow + ((sv >> 8) & 0xffu), v[u] * x[u].y);
+        A::add(arow + ((sv >> 16) & 0xffu), v[u] * x[u].z);
+        A::add(arow + (sv >> 24), v[u] * x[u].w);
+      }
+    }
+  }
+}
+
 // Column phases: all work-groups of one launch gather from the same 1/B of the CBSR table
 // (phase b = source columns [b*NC/B, (b+1)*NC/B)), so the records they touch stay in L2
 // (tools/ubench_gather.hip: ~300 vs ~63 G edges/s for a shared window vs the whole table).
@@ -87,17 +135,34 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     int phases, int phase, const uint32_t* __restrict__ cr, const float* __restrict__ fval,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
     const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
-    int tile_rows) {
+    int tile_rows, int rot_ticks) {
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
   T* acc = reinterpret_cast<T*>(smem_d);
   // Work-group w runs tasks w, w + G, ... (G = grid size; G = #tasks by default, or the
   // resident capacity with the fwd_persistent option, which measured slower on Reddit).
+  // rot_ticks > 0: one launch, each task's sweep rotated to start at the window of the
+  // shared 100 MHz clock, so concurrently running tiles gather from the same columns.
   for (int ti = blockIdx.x; ti < ntasks; ti += gridDim.x) {
   FwdTask t = tasks[ti];
+  int emid = -1;
+  __shared__ int s_w0;
+  if (rot_ticks > 0) {
+    // start the column-sorted sweep at the window the clock points to, wrapping around
+    // (read once per work-group: every wave must split the task at the same edge)
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_w0 = (int)((__builtin_amdgcn_s_memrealtime() / (uint64_t)rot_ticks) % (uint64_t)phases);
+    __syncthreads();
+    const int w0 = s_w0;
+    t.e0 = phase_off[ti * (phases + 1)];
+    t.e1 = phase_off[ti * (phases + 1) + phases];
+    emid = phase_off[ti * (phases + 1) + w0];
+  } else {
   t.e0 = phase_off[ti * (phases + 1) + phase];
   t.e1 = phase_off[ti * (phases + 1) + phase + 1];
+  }
   if (phase > 0 && t.e0 == t.e1) continue;  // nothing to add in this phase (uniform)
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
@@ -127,38 +192,14 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     // chain (col, val) -> CBSR record -> LDS has two dependent global round trips, so
     // memory-level parallelism comes from U independent sub-steps per wave. Out-of-range
     // lanes load a clamped (valid) edge and skip the update.
-    const int last = t.e1 - 1;
-    for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
-      uint32_t cw[U];
-      float v[U];
-      bool ok[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = base + u * EPS + slot;
-        ok[u] = lane_on && e < t.e1;
-        const int ec = ok[u] ? e : last;
-        cw[u] = cr[ec];
-        v[u] = fval[ec];
-      }
-      float4 x[U];
-      uint32_t sel[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint8_t* rp = rec + (size_t)(cw[u] & kFwdColMask) * rec_bytes;
-        x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
-        sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (ok[u]) {
-          T* arow = acc + (cw[u] >> kFwdColBits) * D;
-          const uint32_t sv = sel[u];
-          A::add(arow + (sv & 0xffu), v[u] * x[u].x);
-          A::add(arow + ((sv >> 8) & 0xffu), v[u] * x[u].y);
-          A::add(arow + ((sv >> 16) & 0xffu), v[u] * x[u].z);
-          A::add(arow + (sv >> 24), v[u] * x[u].w);
-        }
-      }
+    if (emid >= 0) {
+      fwd_edges4<U, A>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+                       rec_bytes, D, k);
+      fwd_edges4<U, A>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+                       rec_bytes, D, k);
+    } else {
+      fwd_edges4<U, A>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+                       rec_bytes, D, k);
     }
   } else {
     for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
@@ -544,6 +585,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
                        plan->fwd_rec, plan->num_cols, k, rec_bytes);
     MAXK_LAUNCH_CHECK("pack_cbsr launch");
   }
+  const int rot = plan->fwd_rot_ticks;
   const dim3 block(kFwdThreads);
   // persistent grid: as many work-groups as fit on the device at once (capped by tasks)
 #define FWD_LAUNCH1(V, A, UU)                                                             \
@@ -555,11 +597,11 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
     const int g = plan->fwd_persistent                                                    \
                       ? std::max(1, std::min(plan->n_fwd_tasks, std::max(per_cu, 1) * plan->cus)) \
                       : plan->n_fwd_tasks;                                                \
-    for (int b = 0; b < B; ++b)                                                           \
+    for (int b = 0; b < (rot ? 1 : B); ++b)                                               \
       hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU>), dim3(g), block, lds, s, plan->fwd_tasks, \
                          plan->n_fwd_tasks, plan->fwd_phase_off, B, b, plan->fwd_cr,       \
                          plan->fwd_val, sp_data, sp_index, plan->fwd_rec, rec_bytes, out,  \
-                         D, k, R);                                                         \
+                         D, k, R, rot);                                                    \
   } while (0)
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \

@@ -63,6 +63,8 @@ class PlanOptions(ctypes.Structure):
         ("bwd_min_task_edges", _i32),
         ("bwd_acc_pad", _i32),
         ("bwd_sel_lds", _i32),
+        ("fwd_rotate", _i32),
+        ("reserved", _i32 * 3),
     ]
 
 
