@@ -21,7 +21,7 @@ constexpr int kBwdThreads = 512;        // 8 waves
 constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
 constexpr int kFwdUnroll = 8;           // independent sub-steps in flight per wave
 constexpr int kBwdUnroll = 8;
-constexpr int kBwdTasksPerCu = 8;
+constexpr int kBwdTasksPerCu = 2;
 constexpr int kBwdMinTaskEdges = 16384;  // a chunk's flush costs ~as much as ~4k edges
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
@@ -29,7 +29,7 @@ constexpr double kFwdSlotEdgeRate = 1.5e8;  // edges/s one forward work-group sl
 constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (S = 2, 4 measured slower)
 // Records past the end of the backward edge list that a wave may read (and ignore).
 constexpr int kBwdRecPad = (kBwdThreads / kWave) * kWave * 16 + kWave;  // MI355X: 8 XCDs, work-groups dealt round-robin (speed only)
-constexpr int kBwdLdsBudget = 150 * 1024; // one 512-thread work-group per CU
+constexpr int kBwdLdsBudget = 160 * 1024; // all of a CU's LDS: one 512-thread work-group per CU
 
 // Thread-local error message plumbing for maxk_last_error().
 void set_error(const std::string& msg);

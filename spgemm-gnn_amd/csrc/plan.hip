@@ -520,8 +520,11 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   const bool xcd_order = o.bwd_order == 0;
   int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
   if (xcd_order && nblocks >= kXcds) {
-    // a multiple of the XCD count, so every XCD owns the same number of column blocks
-    nblocks = (nblocks + kXcds - 1) / kXcds * kXcds;
+    // a multiple of the XCD count, so every XCD owns the same number of column blocks; and
+    // of 8 per XCD when that many blocks are needed anyway (measured: 64 / 128 / 256 blocks
+    // for k = 8 / 16 / 32 on Reddit ran 10-25 % faster than 72 / 120 / 240)
+    const int q = nblocks >= kXcds * 8 ? kXcds * 8 : kXcds;
+    nblocks = (nblocks + q - 1) / q * q;
     C = (NC + nblocks - 1) / nblocks;
     nblocks = (NC + C - 1) / C;
   }
