@@ -195,6 +195,7 @@ static void free_plan(maxk_plan* p) {
   dfree(p->bwd_val);
   dfree(p->bwd_rec);
   dfree(p->bwd_sel);
+  dfree(p->bwd_colptr);
   delete p;
 }
 
@@ -294,6 +295,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                      (o.bwd_unroll == 0 || o.bwd_unroll == 4 || o.bwd_unroll == 8 ||
                       o.bwd_unroll == 12 || o.bwd_unroll == 16),
                  "maxk_plan_create: unroll must be 0, 8 or 16 (backward also 4 or 12)");
+  MAXK_CHECK_ARG(o.bwd_algo >= 0 && o.bwd_algo <= 2,
+                 "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks) or 2 (CSC)");
   MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 2,
                  "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_sel_lds >= 0 && o.bwd_sel_lds <= 2,
@@ -517,7 +520,22 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   const int col_bytes = p->bwd_ks * (int)acc_bytes(p->bwd_acc) + (p->bwd_sel_lds ? nslots : 0);
   int C = std::max(1, (lds_budget - 16) / col_bytes);
   C = std::min(C, std::max(NC, 1));
-  const bool xcd_order = o.bwd_order == 0;
+  // Column-major (CSC) backward, option bwd_algo = 2: one wave per column sums its in-edges
+  // in registers (C = 1: the block sort becomes a column sort). Measured slower than the
+  // column blocks on every graph tried, sparse ones included (ogbn-products k = 32: 17.0 vs
+  // 15.0 ms): a block sweeps its edges in row order, so the work-groups resident together
+  // walk the rows of G in near lock-step and share its lines in L2 and the MALL (PMC: L2 hit
+  // 10-43 % vs 2 % for CSC, 7.0 vs 8.0 L2 misses per edge); a column's in-edges come from
+  // anywhere. Kept as an option for that comparison.
+  const int Lc = k / p->bwd_feats;  // lanes per edge of the column-major kernel
+  const bool csc_ok = E > 0 && k % p->bwd_feats == 0 && (Lc & (Lc - 1)) == 0 && Lc <= kWave &&
+                      (uint64_t)N * (uint64_t)D * 4u <= 0xffffffffull;
+  p->bwd_csc = csc_ok && o.bwd_algo == 2;
+  if (p->bwd_csc) {
+    C = 1;
+    p->bwd_sel_lds = 0;
+  }
+  const bool xcd_order = o.bwd_order == 0 && !p->bwd_csc;
   int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
   if (xcd_order && nblocks >= kXcds) {
     // a multiple of the XCD count, so every XCD owns the same number of column blocks; and
@@ -530,7 +548,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   }
   p->bwd_block_cols = C;
   p->n_bwd_blocks = nblocks;
-  std::vector<int64_t> offs(nblocks + 1, 0);
+  std::vector<int64_t> offs(p->bwd_csc ? 1 : nblocks + 1, 0);
   if (E > 0) {
     if (!row_of) {
       PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
@@ -563,17 +581,25 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     hipLaunchKernelGGL(key_offsets_kernel, dim3(nblocks / 256 + 1), dim3(256), 0, s, keys_out,
                        E, nblocks, reinterpret_cast<int32_t*>(d_offs));
     PLAN_TRY(hipGetLastError());
-    std::vector<int32_t> offs32(nblocks + 1);
-    PLAN_TRY(hipMemcpyAsync(offs32.data(), d_offs, sizeof(int32_t) * (nblocks + 1),
-                            hipMemcpyDeviceToHost, s));
     int bad = 0;
     PLAN_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
-    PLAN_TRY(hipStreamSynchronize(s));
+    if (p->bwd_csc) {
+      // column pointers of the column-sorted edge list stay on the device
+      p->bwd_colptr = reinterpret_cast<int32_t*>(d_offs);
+      d_offs = nullptr;
+      p->device_bytes += sizeof(int32_t) * (nblocks + 1);
+      PLAN_TRY(hipStreamSynchronize(s));
+    } else {
+      std::vector<int32_t> offs32(nblocks + 1);
+      PLAN_TRY(hipMemcpyAsync(offs32.data(), d_offs, sizeof(int32_t) * (nblocks + 1),
+                              hipMemcpyDeviceToHost, s));
+      PLAN_TRY(hipStreamSynchronize(s));
+      for (int b = 0; b <= nblocks; ++b) offs[b] = offs32[b];
+    }
     if (bad) {
       set_error("maxk_plan_create: idx contains column ids outside [0, num_cols)");
       return fail(MAXK_ERR_INVALID_ARG);
     }
-    for (int b = 0; b <= nblocks; ++b) offs[b] = offs32[b];
   }
   const int64_t target_tasks = (int64_t)(o.bwd_tasks_per_cu ? o.bwd_tasks_per_cu : kBwdTasksPerCu) * cus;
   const int chunks = (int)std::max<int64_t>(
@@ -581,7 +607,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   const int64_t min_task_edges = o.bwd_min_task_edges > 0 ? o.bwd_min_task_edges : kBwdMinTaskEdges;
   std::vector<BwdTask> btasks;
   int nshared = 0;
-  if (xcd_order && E > 0 && nblocks > 0) {
+  if (p->bwd_csc) {
+    // no tasks: the column-major kernel runs one wave per column
+  } else if (xcd_order && E > 0 && nblocks > 0) {
     // Row-chunk-major, XCD-aware order. Chunk j of every block covers the same rows
     // [R_j, R_j+1) (equal edge counts over the whole graph), so the work-groups that run
     // together sweep the same rows of G and share its lines in their XCD's L2. Work-groups
@@ -675,13 +703,14 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     p->device_bytes += sizeof(BwdTask) * btasks.size();
   }
   // packed backward path: records instead of the three parallel arrays
-  if (packed) {
+  if (packed || p->bwd_csc) {
     PLAN_TRY(hipMalloc(&p->bwd_rec, sizeof(uint32_t) * 3 * (size_t)(E + kBwdRecPad)));
     PLAN_TRY(hipMemsetAsync(p->bwd_rec + 3 * E, 0, sizeof(uint32_t) * 3 * kBwdRecPad, s));
     hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, nullptr,
                        p->bwd_row, p->bwd_col, p->bwd_val, E, C, D, p->bwd_rec);
     PLAN_TRY(hipGetLastError());
-    PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)std::max(NC, 1) * k));
+    if (!p->bwd_csc || p->bwd_feats == 4)
+      PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)std::max(NC, 1) * k));
     PLAN_TRY(hipStreamSynchronize(s));
     dfree(p->bwd_row);
     dfree(p->bwd_col);
@@ -736,6 +765,7 @@ extern "C" int maxk_plan_get_info(const maxk_plan* p, maxk_plan_info* info) {
   info->bwd_tasks = p->n_bwd_tasks;
   info->bwd_shared_blocks = p->n_bwd_shared;
   info->device_bytes = p->device_bytes;
+  info->bwd_algo = p->bwd_csc ? 2 : 1;
   return MAXK_OK;
 }
 

@@ -499,6 +499,77 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
   }
 }
 
+// Column-major backward for sparse graphs (plan->bwd_csc): the records are sorted by column
+// (stable, so rows ascend within a column) and one wavefront owns a column c. Its L = k/F
+// lanes per edge (F = 4: interleaved slots q + L*i from the packed selector word; F = 1: one
+// slot per lane straight from sp_index) load the column's selectors once, then the wave
+// walks the column's edges 64/L at a time, gathering k features of each source row of
+// grad_out and summing them in registers; a shuffle-xor reduction over the edge slots leaves
+// the k sums in lanes 0..L-1, which store them. No LDS, no atomics, no memset: every column
+// is written exactly once.
+template <int F, int U>
+__global__ __launch_bounds__(256) void sspmm_bwd_csc_kernel(
+    const int32_t* __restrict__ colptr, const uint32_t* __restrict__ rec,
+    const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
+    const uint8_t* __restrict__ sp_index, float* __restrict__ grad_sp, int ncols, int k) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int c = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
+  if (c >= ncols) return;
+  const int L = k / F;  // power of two <= 64 (checked by the plan)
+  const int EPS = kWave / L;
+  const int slot = lane / L;
+  const int q = lane - slot * L;
+  uint32_t so[F];
+  if constexpr (F == 4) {
+    const uint32_t s = sel[(size_t)c * L + q];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) so[i] = ((s >> (8 * i)) & 0xffu) << 2;
+  } else {
+    so[0] = (uint32_t)sp_index[(size_t)c * k + q] << 2;
+  }
+  const int e0 = colptr[c], e1 = colptr[c + 1];
+  const __amdgpu_buffer_rsrc_t gr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
+  float acc[F];
+#pragma unroll
+  for (int i = 0; i < F; ++i) acc[i] = 0.f;
+  for (int base = e0; base < e1; base += EPS * U) {
+    uint32_t go[U];
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * EPS + slot;
+      if (e < e1) {
+        const uint3 r3 = *reinterpret_cast<const uint3*>(rec + 3 * (size_t)e);
+        go[u] = r3.x;
+        v[u] = __uint_as_float(r3.z);
+      } else {
+        go[u] = 0;
+        v[u] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = base + u * EPS + slot < e1;
+#pragma unroll
+      for (int i = 0; i < F; ++i) {
+        // out-of-range offset for the idle slots: the buffer load returns 0 (no 0 * inf)
+        const uint32_t off = ok ? go[u] + so[i] : 0xfffffffcu;
+        acc[i] = fmaf(v[u], __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0)), acc[i]);
+      }
+    }
+  }
+  for (int m = L; m < kWave; m <<= 1) {
+#pragma unroll
+    for (int i = 0; i < F; ++i) acc[i] += __shfl_xor(acc[i], m, kWave);
+  }
+  if (slot == 0) {
+    float* dst = grad_sp + (size_t)c * k + q;
+#pragma unroll
+    for (int i = 0; i < F; ++i) dst[i * L] = acc[i];
+  }
+}
+
 // --------------------------------------------------------------------------------------
 // dense CSR SpMM comparator: one wavefront per destination row, 4 features per lane.
 // --------------------------------------------------------------------------------------
@@ -635,6 +706,31 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   if (N == 0) return MAXK_OK;
   MAXK_CHECK_ARG(grad_out && sp_index && grad_sp, "maxk_sspmm_backward: null pointer");
   hipStream_t s = (hipStream_t)stream;
+  if (plan->bwd_csc) {
+    const int F = plan->bwd_feats;
+    if (F == 4) {
+      const int nsel = plan->num_cols * (k / 4);
+      hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
+                         plan->num_cols, k, 1, plan->bwd_sel);
+    }
+    const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
+    const dim3 cgrid((plan->num_cols + 3) / 4);
+#define CSC_LAUNCH(FF, UU)                                                                \
+    hipLaunchKernelGGL((sspmm_bwd_csc_kernel<FF, UU>), cgrid, dim3(256), 0, s,            \
+                       plan->bwd_colptr, plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, \
+                       sp_index, grad_sp, plan->num_cols, k)
+    if (F == 4) {
+      if (plan->bwd_unroll >= 8) CSC_LAUNCH(4, 8);
+      else CSC_LAUNCH(4, 4);
+    } else {
+      if (plan->bwd_unroll >= 16) CSC_LAUNCH(1, 16);
+      else if (plan->bwd_unroll >= 8) CSC_LAUNCH(1, 8);
+      else CSC_LAUNCH(1, 4);
+    }
+#undef CSC_LAUNCH
+    MAXK_LAUNCH_CHECK("sspmm_bwd_csc launch");
+    return MAXK_OK;
+  }
   if (plan->n_bwd_shared > 0)
     MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)plan->num_cols * k * sizeof(float), s));
   if (plan->n_bwd_tasks == 0) return MAXK_OK;

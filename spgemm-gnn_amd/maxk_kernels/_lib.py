@@ -64,7 +64,8 @@ class PlanOptions(ctypes.Structure):
         ("bwd_acc_pad", _i32),
         ("bwd_sel_lds", _i32),
         ("fwd_rotate", _i32),
-        ("reserved", _i32 * 3),
+        ("bwd_algo", _i32),
+        ("reserved", _i32 * 2),
     ]
 
 
@@ -87,6 +88,7 @@ class PlanInfo(ctypes.Structure):
         ("bwd_shared_blocks", _i32),
         ("device_bytes", _i64),
         ("num_cols", _i32),
+        ("bwd_algo", _i32),
     ]
 
     def as_dict(self):

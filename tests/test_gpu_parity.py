@@ -196,6 +196,28 @@ def test_sspmm_backward_vs_oracle(gpu, gname, d, k):
     assert_close(gs, ref, mag)
 
 
+@pytest.mark.parametrize("gname", list(GRAPHS))
+@pytest.mark.parametrize("k", [4, 8, 16, 32, 64, 24])
+@pytest.mark.parametrize("feats", [4, 1])
+def test_sspmm_backward_csc_vs_oracle(gpu, gname, k, feats):
+    """Column-major backward (bwd_algo=2); k=24 (6 lanes per edge) falls back to the blocks."""
+    p, ix, v = GRAPHS[gname]()
+    n, d = p.size - 1, 256
+    x = graphs.features(n, d, seed=k)
+    g = graphs.features(n, d, seed=k + 1)
+    _, oi = oracle.maxk(x.numpy(), k)
+    ref, mag = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k,
+                        options=dict(bwd_algo=2, bwd_features_per_lane=feats))
+    assert plan.info()["bwd_algo"] == (1 if k == 24 else 2)
+    assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
+    val.mul_(-2.0)                        # refresh_values rewrites the column-major records
+    ref, mag = oracle.sspmm_backward(p, ix, v * -2.0, g.numpy(), oi, with_mag=True)
+    plan.refresh_values(val)
+    assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
+
+
 def test_plan_picks_up_value_changes(gpu):
     p, ix, v = GRAPHS["synthetic"]()
     n = p.size - 1
@@ -273,6 +295,8 @@ PLAN_OPTIONS = [
     dict(bwd_unroll=16), dict(bwd_slot_groups=2), dict(bwd_slot_groups=4),
     dict(bwd_lds_bytes=4096), dict(bwd_tasks_per_cu=1), dict(bwd_acc_pad=2), dict(bwd_sel_lds=2),
     dict(bwd_unroll=4), dict(bwd_unroll=12),
+    dict(bwd_algo=2), dict(bwd_algo=2, bwd_unroll=4),
+    dict(bwd_algo=2, bwd_features_per_lane=1), dict(bwd_algo=2, bwd_features_per_lane=1, bwd_unroll=16),
     # chunked blocks (atomic flush into a memset grad_sp), both task orders
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_order=1),
@@ -301,7 +325,8 @@ def test_plan_options_rejected(gpu):
     p, ix, v = GRAPHS["single_node"]()
     ptr, idx, val = graph_on(gpu, p, ix, v)
     for bad in (dict(fwd_unroll=7), dict(bwd_order=3), dict(bwd_slot_groups=3),
-                dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3)):
+                dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3),
+                dict(bwd_algo=3)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 

@@ -41,9 +41,13 @@ def main():
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--dataset", default="reddit")
     ap.add_argument("--which", default="both", choices=["fwd", "bwd", "both"])
+    ap.add_argument("--graph", default=None, help="N,E of a synthetic graph instead of --dataset")
+    ap.add_argument("--fwd", default=None, help="JSON list of forward option dicts")
+    ap.add_argument("--bwd", default=None, help="JSON list of backward option dicts")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    n, e = graphs.DATASETS[args.dataset]
+    n, e = (tuple(int(x) for x in args.graph.split(",")) if args.graph
+            else graphs.DATASETS[args.dataset])
     ptr, idx = graphs.synthetic_csr(n, e, device=dev)
     val = graphs.sage_mean_values(ptr)
     e = idx.numel()
@@ -58,6 +62,10 @@ def main():
                     dict(fwd_tile_rows=64), dict(fwd_tile_rows=64, fwd_unroll=16)]
     bwd_variants = [dict(bwd_features_per_lane=1)] + [
         dict(bwd_slot_groups=s, bwd_tasks_per_cu=tp) for s, tp in itertools.product((1, 2, 4), (4, 8))]
+    if args.fwd:
+        fwd_variants = json.loads(args.fwd)
+    if args.bwd:
+        bwd_variants = json.loads(args.bwd)
     ref_out = ref_grad = None
     results = []
     if args.which in ("fwd", "both"):
