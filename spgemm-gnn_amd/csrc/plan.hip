@@ -310,6 +310,22 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: bwd_slot_groups must be 0 or a power of two <= 64");
   p->fwd_unroll = o.fwd_unroll ? o.fwd_unroll : kFwdUnroll;
   p->bwd_unroll = o.bwd_unroll ? o.bwd_unroll : kBwdUnroll;
+  MAXK_CHECK_ARG((o.fwd_waves == 0 || o.fwd_waves == 4 || o.fwd_waves == 6 || o.fwd_waves == 8) &&
+                     (o.bwd_waves == 0 || o.bwd_waves == 8 || o.bwd_waves == 12 ||
+                      o.bwd_waves == 16),
+                 "maxk_plan_create: fwd_waves must be 0, 4, 6 or 8 and bwd_waves 0, 8, 12 or 16");
+  MAXK_CHECK_ARG(o.fwd_prefetch >= 0 && o.fwd_prefetch <= 2 && o.bwd_prefetch >= 0 &&
+                     o.bwd_prefetch <= 2 && o.fwd_branchless >= 0 && o.fwd_branchless <= 2,
+                 "maxk_plan_create: fwd_prefetch / bwd_prefetch / fwd_branchless must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.fwd_record_bytes == 0 ||
+                     (o.fwd_record_bytes % 16 == 0 && o.fwd_record_bytes >= 5 * k && k % 4 == 0),
+                 "maxk_plan_create: fwd_record_bytes must be 0 or a multiple of 16 >= 5k");
+  // defaults measured on the Reddit-shaped graph (tools/sweep.py, profiles/r01)
+  p->fwd_waves = o.fwd_waves ? o.fwd_waves : kFwdWaves;
+  p->bwd_waves = o.bwd_waves ? o.bwd_waves : (k >= 32 ? 12 : kBwdWaves);
+  p->fwd_prefetch = o.fwd_prefetch == 1;
+  p->bwd_prefetch = o.bwd_prefetch == 1;
+  p->fwd_branchless = o.fwd_branchless == 0 ? (k >= 16) : (o.fwd_branchless == 1);
   {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -478,7 +494,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   }
 
   if (k % 4 == 0 && NC > 0) {
-    p->fwd_rec_bytes = cbsr_record_bytes(k);
+    p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes : cbsr_record_bytes(k);
     PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)NC * p->fwd_rec_bytes));
     p->device_bytes += (int64_t)NC * p->fwd_rec_bytes;
   }

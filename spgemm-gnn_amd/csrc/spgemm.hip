@@ -33,10 +33,28 @@ namespace maxk {
 template <int ACC>
 struct LdsAcc;
 
+// MAXK_PROBE (tools/ builds only, `make probe`; never in the product library): speed probes
+// with wrong numerics. 1: forward ds_add_u64 of the f64 bits; 2: forward without LDS
+// updates; 3: backward ds_add_u32 of the f32 bits instead of the read + CAS; 4: backward
+// ds_add_f32 (correct sums, timing of the native LDS float atomic).
+#ifndef MAXK_PROBE
+#define MAXK_PROBE 0
+#endif
+
 template <>
 struct LdsAcc<MAXK_ACC_F64> {
   using T = double;
-  static __device__ __forceinline__ void add(double* p, float v) { lds_add(p, (double)v); }
+  static __device__ __forceinline__ void add(double* p, float v) {
+#if MAXK_PROBE == 1
+    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p),
+                           (unsigned long long)__double_as_longlong((double)v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+#elif MAXK_PROBE == 2
+    if (v == 1.2345e-30f) lds_add(p, (double)v);  // practically never: keeps the gathers live
+#else
+    lds_add(p, (double)v);
+#endif
+  }
 };
 
 template <>
@@ -81,8 +99,11 @@ __global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
 // iteration with every load issued before the first LDS update. The chain (col, val) ->
 // CBSR record -> LDS has two dependent global round trips, so memory-level parallelism
 // comes from U independent sub-steps per wave. Out-of-range lanes load a clamped (valid)
-// edge and skip the update.
-template <int U, class A>
+// edge and skip the update. PF: the next iteration's edge words are loaded right after
+// this iteration's record gathers (loads retire in issue order), so the edge stream's HBM
+// latency overlaps the LDS updates.
+// FL bit 0 (kFwdPrefetch): prefetch; bit 1 (kFwdBranchless): idle lanes add 0 instead of branching.
+template <int U, class A, int FL>
 __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, int wave,
                                            int nwaves, int EPS, int slot, int l0, bool lane_on,
                                            const uint32_t* __restrict__ cr,
@@ -90,8 +111,21 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
                                            const uint8_t* __restrict__ rec, int rec_bytes,
                                            int D, int k) {
   using T = typename A::T;
+  constexpr bool PF = (FL & kFwdFlagPrefetch) != 0;
   const int last = e1 - 1;
-  for (int base = e0 + wave * EPS * U; base < e1; base += nwaves * EPS * U) {
+  const int stride = nwaves * EPS * U;
+  int base = e0 + wave * EPS * U;
+  uint32_t cn[U];
+  float vn[U];
+  if (PF) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = min(base + u * EPS + slot, last);
+      cn[u] = cr[e];
+      vn[u] = fval[e];
+    }
+  }
+  for (; base < e1; base += stride) {
     uint32_t cw[U];
     float v[U];
     bool ok[U];
@@ -99,9 +133,14 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
     for (int u = 0; u < U; ++u) {
       const int e = base + u * EPS + slot;
       ok[u] = lane_on && e < e1;
-      const int ec = ok[u] ? e : last;
-      cw[u] = cr[ec];
-      v[u] = fval[ec];
+      if (PF) {
+        cw[u] = cn[u];
+        v[u] = vn[u];
+      } else {
+        const int ec = ok[u] ? e : last;
+        cw[u] = cr[ec];
+        v[u] = fval[ec];
+      }
     }
     float4 x[U];
     uint32_t sel[U];
@@ -111,15 +150,29 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
       x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
       sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
     }
+    if (PF) {  // unconditional (clamped), see sspmm_bwd4_kernel
+      __builtin_amdgcn_sched_barrier(0);  // keep every gather ahead of these loads
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(base + stride + u * EPS + slot, last);
+        cn[u] = cr[e];
+        vn[u] = fval[e];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // Branchless: idle lanes add 0 at their clamped (valid) edge's addresses; with a branch
+    // the compiler sinks sub-step 0's gather below the other loads (measured: faster at
+    // k = 16, slower at k = 8).
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (ok[u]) {
+      if ((FL & kFwdFlagBranchless) || ok[u]) {
         T* arow = acc + (cw[u] >> kFwdColBits) * D;
         const uint32_t sv = sel[u];
-        A::add(arow + (sv & 0xffu), v[u] * x[u].x);
-        A::add(arow + ((sv >> 8) & 0xffu), v[u] * x[u].y);
-        A::add(arow + ((sv >> 16) & 0xffu), v[u] * x[u].z);
-        A::add(arow + (sv >> 24), v[u] * x[u].w);
+        const float vu = (FL & kFwdFlagBranchless) && !ok[u] ? 0.f : v[u];
+        A::add(arow + (sv & 0xffu), vu * x[u].x);
+        A::add(arow + ((sv >> 8) & 0xffu), vu * x[u].y);
+        A::add(arow + ((sv >> 16) & 0xffu), vu * x[u].z);
+        A::add(arow + (sv >> 24), vu * x[u].w);
       }
     }
   }
@@ -129,8 +182,8 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
 // (phase b = source columns [b*NC/B, (b+1)*NC/B)), so the records they touch stay in L2
 // (tools/ubench_gather.hip: ~300 vs ~63 G edges/s for a shared window vs the whole table).
 // Phase 0 stores the task's rows, later phases continue from the stored partial sums.
-template <int VEC, int ACC, int U>
-__global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
+template <int VEC, int ACC, int U, int NT, int FL>
+__global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     const FwdTask* __restrict__ tasks, int ntasks, const int32_t* __restrict__ phase_off,
     int phases, int phase, const uint32_t* __restrict__ cr, const float* __restrict__ fval,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
@@ -170,9 +223,9 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   __syncthreads();  // the previous task's write-back has finished reading acc
   if (phase > 0 && !split) {
     const float* src = out + (size_t)t.row0 * D;
-    for (int i = threadIdx.x; i < n; i += kFwdThreads) acc[i] = T(src[i]);
+    for (int i = threadIdx.x; i < n; i += NT) acc[i] = T(src[i]);
   } else {
-    for (int i = threadIdx.x; i < n; i += kFwdThreads) acc[i] = T(0);
+    for (int i = threadIdx.x; i < n; i += NT) acc[i] = T(0);
   }
   __syncthreads();
 
@@ -185,7 +238,7 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   const int slot = lane / L;
   const int l0 = (lane - slot * L) * VEC;
   const bool lane_on = slot < EPS;
-  constexpr int kWaves = kFwdThreads / kWave;
+  constexpr int kWaves = NT / kWave;
 
   if constexpr (VEC == 4) {
     // U sub-steps per iteration with every load issued before the first LDS update: the
@@ -193,12 +246,12 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     // memory-level parallelism comes from U independent sub-steps per wave. Out-of-range
     // lanes load a clamped (valid) edge and skip the update.
     if (emid >= 0) {
-      fwd_edges4<U, A>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+      fwd_edges4<U, A, FL>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
                        rec_bytes, D, k);
-      fwd_edges4<U, A>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+      fwd_edges4<U, A, FL>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
                        rec_bytes, D, k);
     } else {
-      fwd_edges4<U, A>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+      fwd_edges4<U, A, FL>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
                        rec_bytes, D, k);
     }
   } else {
@@ -218,14 +271,14 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   float* dst = out + (size_t)t.row0 * D;
   if (!split) {
     if ((D & 3) == 0) {
-      for (int i = threadIdx.x * 4; i < n; i += kFwdThreads * 4)
+      for (int i = threadIdx.x * 4; i < n; i += NT * 4)
         *reinterpret_cast<float4*>(dst + i) =
             make_float4((float)acc[i], (float)acc[i + 1], (float)acc[i + 2], (float)acc[i + 3]);
     } else {
-      for (int i = threadIdx.x; i < n; i += kFwdThreads) dst[i] = (float)acc[i];
+      for (int i = threadIdx.x; i < n; i += NT) dst[i] = (float)acc[i];
     }
   } else {
-    for (int i = threadIdx.x; i < D; i += kFwdThreads) global_add(dst + i, (float)acc[i]);
+    for (int i = threadIdx.x; i < D; i += NT) global_add(dst + i, (float)acc[i]);
   }
   }  // task loop
 }
@@ -384,8 +437,12 @@ __global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int n, int
            ((uint32_t)s[3 * L] << 24);
 }
 
-template <int U>
-__global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
+// NT threads per work-group (8, 12 or 16 waves: more waves, more gathers in flight per CU
+// under the same LDS block). PF: the next sub-steps' records are loaded right after this
+// step's gathers are issued, so the record stream's HBM latency overlaps the LDS updates
+// (loads retire in issue order, so they must not precede the gathers the updates wait on).
+template <int U, int NT, bool PF>
+__global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
     float* __restrict__ grad_sp, int k, int S, int ncols_all, int KS, int sel_lds) {
@@ -396,14 +453,14 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
   const int ns = k / S;  // slots of this group: [t.group * ns, (t.group + 1) * ns)
   const int L = ns >> 2;  // lanes per edge, 4 slots each: q, q + L, q + 2L, q + 3L
   const int nacc = t.ncols * KS;
-  for (int i = threadIdx.x; i < nacc; i += kBwdThreads) bacc[i] = 0.f;
+  for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
   // sel_lds: the block's selector words are staged in LDS behind the accumulator, so the
   // per-edge selector lookup is an LDS read instead of an L1 miss (the G rows evict the
   // block's 16 B/column table from the 32 KB L1)
   const uint32_t* selg = sel + ((size_t)t.group * ncols_all + t.col0) * L;
   uint32_t* sell = reinterpret_cast<uint32_t*>(bacc) + ((nacc + 3) & ~3);
   if (sel_lds)
-    for (int i = threadIdx.x; i < t.ncols * L; i += kBwdThreads) sell[i] = selg[i];
+    for (int i = threadIdx.x; i < t.ncols * L; i += NT) sell[i] = selg[i];
   __syncthreads();
 
   const int EPS = kWave / L;
@@ -412,21 +469,30 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
   const int slot = lane / L;
   const int q = lane - slot * L;
   const bool lane_on = slot < EPS;
-  constexpr int kWaves = kBwdThreads / kWave;
+  constexpr int kWaves = NT / kWave;
+  const int stride = kWaves * EPS * U;
   const __amdgpu_buffer_rsrc_t gr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
   const uint32_t* selb = (sel_lds ? sell : selg) + q;
   unsigned* accq = reinterpret_cast<unsigned*>(bacc) + q;
+  const uint3* rec3 = reinterpret_cast<const uint3*>(rec);
 
-  for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
+  // records past e1 (a padded or neighbouring record) are loaded and ignored
+  int base = t.e0 + wave * EPS * U;
+  uint3 rn[U];
+  if (PF) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) rn[u] = rec3[min(base + u * EPS + slot, t.e1 - 1)];
+  }
+  for (; base < t.e1; base += stride) {
     uint32_t go[U], cl[U];
     float v[U];
     bool ok[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int e = base + u * EPS + slot;  // past e1: a padded or neighbouring record
+      const int e = base + u * EPS + slot;
       ok[u] = lane_on && e < t.e1;
-      const uint3 r3 = *reinterpret_cast<const uint3*>(rec + 3 * (size_t)e);
+      const uint3 r3 = PF ? rn[u] : rec3[e];
       go[u] = r3.x;
       cl[u] = r3.y;
       v[u] = __uint_as_float(r3.z);
@@ -440,9 +506,37 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t off = go[u] + (((s[u] >> (8 * i)) & 0xffu) << 2);
-        x[u][i] = v[u] * __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
+        x[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
       }
     }
+    if (PF) {  // unconditional (clamped): a branch here would make the updates below wait
+               // for these loads too (vmcnt counts both paths)
+      __builtin_amdgcn_sched_barrier(0);  // keep every gather ahead of these loads
+#pragma unroll
+      for (int u = 0; u < U; ++u) rn[u] = rec3[min(base + stride + u * EPS + slot, t.e1 - 1)];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[u][i] *= v[u];
+#if MAXK_PROBE == 3 || MAXK_PROBE == 4
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      unsigned* a = accq + cl[u] * KS;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (ok[u]) {
+          if (MAXK_PROBE == 3)
+            __hip_atomic_fetch_add(a + i * L, __float_as_uint(x[u][i]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+          else
+            __hip_atomic_fetch_add(reinterpret_cast<float*>(a + i * L), x[u][i],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    continue;
+#endif
     unsigned old[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -490,7 +584,7 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd4_kernel(
 
   float* dst = grad_sp + (size_t)t.col0 * k + t.group * ns;
   const int n = t.ncols * ns;
-  for (int i = threadIdx.x; i < n; i += kBwdThreads) {
+  for (int i = threadIdx.x; i < n; i += NT) {
     const int c = i / ns;
     const int l = i - c * ns;
     const float a = bacc[c * KS + l];
@@ -657,35 +751,51 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
     MAXK_LAUNCH_CHECK("pack_cbsr launch");
   }
   const int rot = plan->fwd_rot_ticks;
-  const dim3 block(kFwdThreads);
   // persistent grid: as many work-groups as fit on the device at once (capped by tasks)
-#define FWD_LAUNCH1(V, A, UU)                                                             \
+#define FWD_LAUNCH1(V, A, UU, NT, FL)                                                     \
   do {                                                                                    \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, A, UU>, lds));      \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, A, UU, NT, FL>, lds)); \
     int per_cu = 0;                                                                       \
     MAXK_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(                            \
-        &per_cu, spgemm_fwd_kernel<V, A, UU>, kFwdThreads, lds));                         \
+        &per_cu, spgemm_fwd_kernel<V, A, UU, NT, FL>, NT, lds));                          \
     const int g = plan->fwd_persistent                                                    \
                       ? std::max(1, std::min(plan->n_fwd_tasks, std::max(per_cu, 1) * plan->cus)) \
                       : plan->n_fwd_tasks;                                                \
     for (int b = 0; b < (rot ? 1 : B); ++b)                                               \
-      hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU>), dim3(g), block, lds, s, plan->fwd_tasks, \
-                         plan->n_fwd_tasks, plan->fwd_phase_off, B, b, plan->fwd_cr,       \
-                         plan->fwd_val, sp_data, sp_index, plan->fwd_rec, rec_bytes, out,  \
-                         D, k, R, rot);                                                    \
+      hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU, NT, FL>), dim3(g), dim3(NT), lds, s, \
+                         plan->fwd_tasks, plan->n_fwd_tasks, plan->fwd_phase_off, B, b,   \
+                         plan->fwd_cr, plan->fwd_val, sp_data, sp_index, plan->fwd_rec,   \
+                         rec_bytes, out, D, k, R, rot);                                   \
   } while (0)
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \
-    if (plan->fwd_unroll == 16) FWD_LAUNCH1(V, A, 16);                                    \
-    else FWD_LAUNCH1(V, A, 8);                                                            \
+    if (plan->fwd_unroll == 16) FWD_LAUNCH1(V, A, 16, 256, 0);                            \
+    else FWD_LAUNCH1(V, A, 8, 256, 0);                                                    \
   } while (0)
-  if (k % 4 == 0) {
+#define FWD_LAUNCH_FL(NT)                                                                 \
+  do {                                                                                    \
+    switch (FL) {                                                                         \
+      case 0: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 0); break;                              \
+      case 1: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 1); break;                              \
+      case 2: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 2); break;                              \
+      default: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 3); break;                             \
+    }                                                                                     \
+  } while (0)
+  const int W = plan->fwd_waves;
+  const int FL = (plan->fwd_prefetch ? kFwdFlagPrefetch : 0) |
+                 (plan->fwd_branchless ? kFwdFlagBranchless : 0);
+  if (k % 4 == 0 && plan->fwd_acc == MAXK_ACC_F64 && plan->fwd_unroll == 8) {
+    if (W == 8) FWD_LAUNCH_FL(512);
+    else if (W == 6) FWD_LAUNCH_FL(384);
+    else FWD_LAUNCH_FL(256);
+  } else if (k % 4 == 0) {
     if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(4, MAXK_ACC_F32_CAS);
     else FWD_LAUNCH(4, MAXK_ACC_F64);
   } else {
     if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(1, MAXK_ACC_F32_CAS);
     else FWD_LAUNCH(1, MAXK_ACC_F64);
   }
+#undef FWD_LAUNCH_FL
 #undef FWD_LAUNCH
 #undef FWD_LAUNCH1
   MAXK_LAUNCH_CHECK("spgemm_fwd launch");
@@ -735,7 +845,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)plan->num_cols * k * sizeof(float), s));
   if (plan->n_bwd_tasks == 0) return MAXK_OK;
   const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k, plan->bwd_acc);
-  const dim3 grid(plan->n_bwd_tasks), block(kBwdThreads);
+  const dim3 grid(plan->n_bwd_tasks), block(kBwdThreads);  // general path: 512 threads
   if (plan->bwd_rec) {
     const int S = plan->bwd_slot_groups;
     const int nsel = plan->num_cols * (k / 4);
@@ -744,17 +854,27 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
     const size_t lds4 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
                         (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
-#define BWD4_LAUNCH(UU)                                                                   \
+#define BWD4_LAUNCH(UU, NT, PF)                                                           \
     do {                                                                                  \
-      if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU>, lds4));         \
-      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU>), grid, block, lds4, s, plan->bwd_tasks,  \
-                         plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, grad_sp, k, S,  \
-                         plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds);                \
+      if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, PF>, lds4)); \
+      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF>), grid, dim3(NT), lds4, s,        \
+                         plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, \
+                         grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds); \
     } while (0)
-    if (plan->bwd_unroll == 16) BWD4_LAUNCH(16);
-    else if (plan->bwd_unroll == 12) BWD4_LAUNCH(12);
-    else if (plan->bwd_unroll == 4) BWD4_LAUNCH(4);
-    else BWD4_LAUNCH(8);
+    const int W = plan->bwd_waves, U = plan->bwd_unroll;
+    const bool PFon = plan->bwd_prefetch != 0;
+    if (W == 16) {
+      if (PFon) BWD4_LAUNCH(6, 1024, true);
+      else BWD4_LAUNCH(6, 1024, false);
+    } else if (W == 12) {
+      if (PFon) BWD4_LAUNCH(8, 768, true);
+      else BWD4_LAUNCH(8, 768, false);
+    } else if (PFon) {
+      BWD4_LAUNCH(8, 512, true);
+    } else if (U == 16) BWD4_LAUNCH(16, 512, false);
+    else if (U == 12) BWD4_LAUNCH(12, 512, false);
+    else if (U == 4) BWD4_LAUNCH(4, 512, false);
+    else BWD4_LAUNCH(8, 512, false);
 #undef BWD4_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd launch");
     return MAXK_OK;

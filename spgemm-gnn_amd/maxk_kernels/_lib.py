@@ -65,6 +65,12 @@ class PlanOptions(ctypes.Structure):
         ("bwd_sel_lds", _i32),
         ("fwd_rotate", _i32),
         ("bwd_algo", _i32),
+        ("fwd_waves", _i32),
+        ("bwd_waves", _i32),
+        ("fwd_prefetch", _i32),
+        ("bwd_prefetch", _i32),
+        ("fwd_record_bytes", _i32),
+        ("fwd_branchless", _i32),
         ("reserved", _i32 * 2),
     ]
 

@@ -302,6 +302,12 @@ PLAN_OPTIONS = [
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_order=1),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_slot_groups=2),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_accumulator="f64"),
+    # wavefronts per work-group, edge-stream prefetch, branchless idle lanes, record stride
+    dict(fwd_waves=6), dict(fwd_waves=8, fwd_prefetch=1), dict(fwd_prefetch=1),
+    dict(fwd_branchless=1), dict(fwd_branchless=2), dict(fwd_record_bytes=256),
+    dict(bwd_waves=12), dict(bwd_waves=16), dict(bwd_prefetch=1),
+    dict(bwd_waves=12, bwd_prefetch=1), dict(bwd_waves=16, bwd_prefetch=1),
+    dict(bwd_waves=12, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
 ]
 
 
@@ -326,7 +332,8 @@ def test_plan_options_rejected(gpu):
     ptr, idx, val = graph_on(gpu, p, ix, v)
     for bad in (dict(fwd_unroll=7), dict(bwd_order=3), dict(bwd_slot_groups=3),
                 dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3),
-                dict(bwd_algo=3)):
+                dict(bwd_algo=3), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
+                dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 
