@@ -25,6 +25,7 @@ constexpr int kFwdWaves = 4;            // default wavefronts per forward work-g
 constexpr int kBwdWaves = 8;            // default wavefronts per backward work-group
 constexpr int kFwdFlagPrefetch = 1;     // forward kernel flags (template FL)
 constexpr int kFwdFlagBranchless = 2;
+constexpr int kFwdFlagChunk3 = 4;
 constexpr int kBwdTasksPerCu = 2;
 constexpr int kBwdMinTaskEdges = 16384;  // a chunk's flush costs ~as much as ~4k edges
 constexpr int kXcds = 8;
@@ -142,6 +143,7 @@ struct maxk_plan {
   int32_t bwd_waves = 8;         // wavefronts per backward work-group
   int32_t fwd_prefetch = 0;      // next sub-steps' edge words loaded during the gathers
   int32_t fwd_branchless = 1;    // idle lanes add 0 instead of branching around the update
+  int32_t fwd_chunk3 = 0;        // lane-chunk records: 3 values + their selectors per 16 B
   int32_t bwd_prefetch = 0;
   int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per phase
   int32_t* fwd_perm = nullptr;   // CSR edge id of each permuted forward edge

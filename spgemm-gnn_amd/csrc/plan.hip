@@ -318,14 +318,20 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                      o.bwd_prefetch <= 2 && o.fwd_branchless >= 0 && o.fwd_branchless <= 2,
                  "maxk_plan_create: fwd_prefetch / bwd_prefetch / fwd_branchless must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.fwd_record_bytes == 0 ||
-                     (o.fwd_record_bytes % 16 == 0 && o.fwd_record_bytes >= 5 * k && k % 4 == 0),
+                     (o.fwd_record_bytes % 16 == 0 &&
+                      (o.fwd_chunk3 == 1 || (o.fwd_record_bytes >= 5 * k && k % 4 == 0))),
                  "maxk_plan_create: fwd_record_bytes must be 0 or a multiple of 16 >= 5k");
   // defaults measured on the Reddit-shaped graph (tools/sweep.py, profiles/r01)
   p->fwd_waves = o.fwd_waves ? o.fwd_waves : kFwdWaves;
   p->bwd_waves = o.bwd_waves ? o.bwd_waves : (k >= 32 ? 12 : kBwdWaves);
   p->fwd_prefetch = o.fwd_prefetch == 1;
   p->bwd_prefetch = o.bwd_prefetch == 1;
-  p->fwd_branchless = o.fwd_branchless == 0 ? (k >= 16) : (o.fwd_branchless == 1);
+  MAXK_CHECK_ARG(o.fwd_chunk3 >= 0 && o.fwd_chunk3 <= 2, "maxk_plan_create: fwd_chunk3 must be 0, 1 or 2");
+  // lane-chunk records by default where the 4-values-per-lane layout fits k badly (Reddit:
+  // k = 8 0.95 vs 1.02 ms, k = 24 1.93 vs 2.09 ms; k = 16 / 32 / 64 are slower with chunks),
+  // and for every k % 4 != 0 (the alternative is the 1-feature-per-lane kernel)
+  p->fwd_chunk3 = (o.fwd_chunk3 == 1 || (o.fwd_chunk3 == 0 && k % 16 != 0)) && (k + 2) / 3 <= kWave;
+  p->fwd_branchless = o.fwd_branchless == 0 ? (k >= 16 || p->fwd_chunk3) : (o.fwd_branchless == 1);
   {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -493,7 +499,17 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     p->device_bytes += sizeof(int32_t) * zrows.size();
   }
 
-  if (k % 4 == 0 && NC > 0) {
+  if (p->fwd_chunk3 && NC > 0) {
+    const int b = (k + 2) / 3 * 16;
+    if (o.fwd_record_bytes != 0 && o.fwd_record_bytes < b) {
+      set_error("maxk_plan_create: fwd_record_bytes too small for the lane-chunk records");
+      return fail(MAXK_ERR_INVALID_ARG);
+    }
+    p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes
+                                          : (b <= 64 ? 64 : b <= 128 ? 128 : b);
+    PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)NC * p->fwd_rec_bytes));
+    p->device_bytes += (int64_t)NC * p->fwd_rec_bytes;
+  } else if (k % 4 == 0 && NC > 0) {
     p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes : cbsr_record_bytes(k);
     PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)NC * p->fwd_rec_bytes));
     p->device_bytes += (int64_t)NC * p->fwd_rec_bytes;
@@ -515,7 +531,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   const int lds_budget = o.bwd_lds_bytes ? o.bwd_lds_bytes : kBwdLdsBudget;
   // packed path (sspmm_bwd4_kernel): f32 accumulators, 4 selector slots per lane, grad_out
   // addressable with 32-bit byte offsets
-  const bool packed = E > 0 && k % 4 == 0 && p->bwd_feats == 4 &&
+  // (or sspmm_bwd1_kernel: one slot per lane, k <= 64 lanes per edge)
+  const bool packed = E > 0 && ((k % 4 == 0 && p->bwd_feats == 4) || (p->bwd_feats == 1 && k <= kWave)) &&
                       p->bwd_acc == MAXK_ACC_F32_CAS &&
                       (uint64_t)N * (uint64_t)D * 4u <= 0xffffffffull;
   // Slot groups: the k selector slots are split into S groups of k/S consecutive (sorted,
@@ -523,7 +540,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // few grad_out lines its group's features fall in, and a block spans S times more
   // columns, so more edges share each fetched row (SSpMM is bound by L1-miss requests).
   int S = 1;
-  if (packed) {
+  if (packed && p->bwd_feats == 4) {
     S = o.bwd_slot_groups ? o.bwd_slot_groups : kBwdSlotGroups;
     while (S > 1 && (k % (4 * S)) != 0) S >>= 1;
   }
@@ -725,7 +742,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, nullptr,
                        p->bwd_row, p->bwd_col, p->bwd_val, E, C, D, p->bwd_rec);
     PLAN_TRY(hipGetLastError());
-    if (!p->bwd_csc || p->bwd_feats == 4)
+    if (p->bwd_feats == 4)  // per-call lane-ordered selector words (pack_sel_kernel)
       PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)std::max(NC, 1) * k));
     PLAN_TRY(hipStreamSynchronize(s));
     dfree(p->bwd_row);
@@ -733,7 +750,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     dfree(p->bwd_val);
     p->bwd_row = p->bwd_col = nullptr;
     p->bwd_val = nullptr;
-    p->device_bytes += (int64_t)NC * k + 12ll * kBwdRecPad;  // rec replaces row/col/val
+    p->device_bytes += (p->bwd_feats == 4 ? (int64_t)NC * k : 0) + 12ll * kBwdRecPad;
   }
   PLAN_TRY(hipStreamSynchronize(s));
   dfree(row_of);

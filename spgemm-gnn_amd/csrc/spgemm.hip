@@ -36,7 +36,8 @@ struct LdsAcc;
 // MAXK_PROBE (tools/ builds only, `make probe`; never in the product library): speed probes
 // with wrong numerics. 1: forward ds_add_u64 of the f64 bits; 2: forward without LDS
 // updates; 3: backward ds_add_u32 of the f32 bits instead of the read + CAS; 4: backward
-// ds_add_f32 (correct sums, timing of the native LDS float atomic).
+// ds_add_f32 (correct sums, timing of the native LDS float atomic); 5: backward without LDS
+// updates; 6: backward gathers from grad_out row 0 only (L1 hits); 7: both 5 and 6.
 #ifndef MAXK_PROBE
 #define MAXK_PROBE 0
 #endif
@@ -95,6 +96,33 @@ __global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
   }
 }
 
+// Lane-chunk CBSR records (plan->fwd_chunk3): chunk j of column c is 16 B, {x[3j],
+// x[3j+1], x[3j+2], selectors 3j..3j+2 in bytes 0..2 of the 4th word}, so ONE dwordx4 gather
+// gives a lane its 3 values and their selectors (the 4-values-per-lane records need a
+// second, selector, gather per lane). The gathers are bound by L1 line lookups per
+// instruction, not by bytes (tools/ubench_tcp.hip); padding slots (3j+i >= k) are 0.
+__global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
+                                  const uint8_t* __restrict__ sp_index,
+                                  uint8_t* __restrict__ rec, int ncols, int k, int rec_bytes) {
+  const int chunks = (k + 2) / 3;
+  const int64_t total = (int64_t)ncols * chunks;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = t / chunks;
+    const int j = (int)(t - c * chunks);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int l = 3 * j + i;
+      if (l < k) {
+        w[i] = __float_as_uint(sp_data[c * k + l]);
+        w[3] |= (uint32_t)sp_index[c * k + l] << (8 * i);
+      }
+    }
+    *reinterpret_cast<uint4*>(rec + c * rec_bytes + j * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // One wave's share of the forward edges [e0, e1) (VEC = 4 lanes path): U sub-steps per
 // iteration with every load issued before the first LDS update. The chain (col, val) ->
 // CBSR record -> LDS has two dependent global round trips, so memory-level parallelism
@@ -102,7 +130,8 @@ __global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
 // edge and skip the update. PF: the next iteration's edge words are loaded right after
 // this iteration's record gathers (loads retire in issue order), so the edge stream's HBM
 // latency overlaps the LDS updates.
-// FL bit 0 (kFwdPrefetch): prefetch; bit 1 (kFwdBranchless): idle lanes add 0 instead of branching.
+// FL bit 0 (kFwdFlagPrefetch): prefetch; bit 1 (kFwdFlagBranchless): idle lanes add 0 instead
+// of branching; bit 2 (kFwdFlagChunk3): lane-chunk records (pack_cbsr3_kernel), l0 = chunk.
 template <int U, class A, int FL>
 __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, int wave,
                                            int nwaves, int EPS, int slot, int l0, bool lane_on,
@@ -112,6 +141,7 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
                                            int D, int k) {
   using T = typename A::T;
   constexpr bool PF = (FL & kFwdFlagPrefetch) != 0;
+  constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
   const int last = e1 - 1;
   const int stride = nwaves * EPS * U;
   int base = e0 + wave * EPS * U;
@@ -147,8 +177,14 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint8_t* rp = rec + (size_t)(cw[u] & kFwdColMask) * rec_bytes;
-      x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
-      sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
+      if constexpr (C3) {  // lane chunk: 3 values + their selector bytes, one gather
+        const uint4 w = *reinterpret_cast<const uint4*>(rp + l0 * 16);
+        x[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), 0.f);
+        sel[u] = w.w;
+      } else {
+        x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
+        sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
+      }
     }
     if (PF) {  // unconditional (clamped), see sspmm_bwd4_kernel
       __builtin_amdgcn_sched_barrier(0);  // keep every gather ahead of these loads
@@ -169,10 +205,17 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
         T* arow = acc + (cw[u] >> kFwdColBits) * D;
         const uint32_t sv = sel[u];
         const float vu = (FL & kFwdFlagBranchless) && !ok[u] ? 0.f : v[u];
-        A::add(arow + (sv & 0xffu), vu * x[u].x);
-        A::add(arow + ((sv >> 8) & 0xffu), vu * x[u].y);
-        A::add(arow + ((sv >> 16) & 0xffu), vu * x[u].z);
-        A::add(arow + (sv >> 24), vu * x[u].w);
+        if constexpr (C3) {
+          // l0 = chunk index: slots 3 l0 .. 3 l0 + 2 (the last chunk may be partly padding)
+          A::add(arow + (sv & 0xffu), vu * x[u].x);
+          if (3 * l0 + 1 < k) A::add(arow + ((sv >> 8) & 0xffu), vu * x[u].y);
+          if (3 * l0 + 2 < k) A::add(arow + ((sv >> 16) & 0xffu), vu * x[u].z);
+        } else {
+          A::add(arow + (sv & 0xffu), vu * x[u].x);
+          A::add(arow + ((sv >> 8) & 0xffu), vu * x[u].y);
+          A::add(arow + ((sv >> 16) & 0xffu), vu * x[u].z);
+          A::add(arow + (sv >> 24), vu * x[u].w);
+        }
       }
     }
   }
@@ -231,12 +274,13 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
 
   // lanes per edge: VEC==4 => k % 4 == 0 and k/4 <= 64; VEC==1 => min(k, 64) lanes that
   // loop over the row's k entries.
-  const int L = (VEC == 4) ? k / 4 : (k < kWave ? k : kWave);
+  constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
+  const int L = (VEC == 4) ? (C3 ? (k + 2) / 3 : k / 4) : (k < kWave ? k : kWave);
   const int EPS = kWave / L;  // edges per wave instruction
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int slot = lane / L;
-  const int l0 = (lane - slot * L) * VEC;
+  const int l0 = (lane - slot * L) * (C3 ? 1 : VEC);
   const bool lane_on = slot < EPS;
   constexpr int kWaves = NT / kWave;
 
@@ -247,12 +291,12 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     // lanes load a clamped (valid) edge and skip the update.
     if (emid >= 0) {
       fwd_edges4<U, A, FL>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
-                       rec_bytes, D, k);
+                           rec_bytes, D, k);
       fwd_edges4<U, A, FL>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
-                       rec_bytes, D, k);
+                           rec_bytes, D, k);
     } else {
       fwd_edges4<U, A, FL>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
-                       rec_bytes, D, k);
+                           rec_bytes, D, k);
     }
   } else {
     for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
@@ -269,16 +313,16 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   __syncthreads();
 
   float* dst = out + (size_t)t.row0 * D;
+  auto get = [&](int i) -> float { return (float)acc[i]; };
   if (!split) {
     if ((D & 3) == 0) {
       for (int i = threadIdx.x * 4; i < n; i += NT * 4)
-        *reinterpret_cast<float4*>(dst + i) =
-            make_float4((float)acc[i], (float)acc[i + 1], (float)acc[i + 2], (float)acc[i + 3]);
+        *reinterpret_cast<float4*>(dst + i) = make_float4(get(i), get(i + 1), get(i + 2), get(i + 3));
     } else {
-      for (int i = threadIdx.x; i < n; i += NT) dst[i] = (float)acc[i];
+      for (int i = threadIdx.x; i < n; i += NT) dst[i] = get(i);
     }
   } else {
-    for (int i = threadIdx.x; i < D; i += NT) global_add(dst + i, (float)acc[i]);
+    for (int i = threadIdx.x; i < D; i += NT) global_add(dst + i, get(i));
   }
   }  // task loop
 }
@@ -505,7 +549,11 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+#if MAXK_PROBE == 6 || MAXK_PROBE == 7
+        const uint32_t off = (((s[u] >> (8 * i)) & 0xffu) << 2);  // row 0 only: L1 hits
+#else
         const uint32_t off = go[u] + (((s[u] >> (8 * i)) & 0xffu) << 2);
+#endif
         x[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
       }
     }
@@ -520,6 +568,17 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[u][i] *= v[u];
+#if MAXK_PROBE == 5 || MAXK_PROBE == 7
+    {
+      float sink = 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sink += x[u][i];
+      if (sink == 1.2345e-30f) accq[0] = 1u;  // practically never: keeps the gathers live
+    }
+    continue;
+#endif
 #if MAXK_PROBE == 3 || MAXK_PROBE == 4
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -590,6 +649,113 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const float a = bacc[c * KS + l];
     if (t.shared) global_add(dst + (size_t)c * k + l, a);
     else dst[(size_t)c * k + l] = a;
+  }
+}
+
+// Packed backward with one selector slot per lane (plan->bwd_feats == 1, k <= 64): the k
+// lanes of an edge gather k dwords of ONE row of grad_out in one instruction, so a wave
+// instruction covers 64/k edges that are mostly of the same row (edges are row-sorted in a
+// block) and touches ~8 lines of G, where the 4-slots-per-lane kernel's instructions cover
+// slot group i of 64/(k/4) edges of ~k/4 rows. The gathers are bound by distinct lines per
+// instruction at the L1 (tools/ubench_tcp.hip), not by lanes. The block's selector bytes are
+// staged in LDS straight from sp_index (no per-call packing).
+template <int U, int NT>
+__global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
+    const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
+    const float* __restrict__ G, uint32_t g_bytes, const uint8_t* __restrict__ sp_index,
+    float* __restrict__ grad_sp, int k, int KS) {
+  extern __shared__ __align__(16) double bsmem[];
+  float* bacc = reinterpret_cast<float*>(bsmem);
+  const BwdTask t = tasks[blockIdx.x];
+  if (t.ncols == 0 || (t.shared && t.e0 == t.e1)) return;  // padding / nothing to add
+  const int nacc = t.ncols * KS;
+  for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
+  uint8_t* sell = reinterpret_cast<uint8_t*>(bacc + ((nacc + 3) & ~3));
+  const uint8_t* selg = sp_index + (size_t)t.col0 * k;
+  const int nsel = t.ncols * k;
+  if ((k & 3) == 0) {
+    for (int i = threadIdx.x; i < nsel / 4; i += NT)
+      reinterpret_cast<uint32_t*>(sell)[i] = reinterpret_cast<const uint32_t*>(selg)[i];
+  } else {
+    for (int i = threadIdx.x; i < nsel; i += NT) sell[i] = selg[i];
+  }
+  __syncthreads();
+
+  const int L = k;  // lanes per edge
+  const int EPS = kWave / L;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int slot = lane / L;
+  const int q = lane - slot * L;
+  const bool lane_on = slot < EPS;
+  constexpr int kWaves = NT / kWave;
+  const int stride = kWaves * EPS * U;
+  const __amdgpu_buffer_rsrc_t gr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
+  const uint3* rec3 = reinterpret_cast<const uint3*>(rec);
+  const uint8_t* selq = sell + q;
+  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + q;
+
+  for (int base = t.e0 + wave * EPS * U; base < t.e1; base += stride) {
+    uint32_t go[U], cl[U];
+    float v[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * EPS + slot;  // past e1: a padded or neighbouring record
+      ok[u] = lane_on && e < t.e1;
+      const uint3 r3 = rec3[e];
+      go[u] = r3.x;
+      cl[u] = r3.y;
+      v[u] = __uint_as_float(r3.z);
+    }
+    float x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t off = go[u] + ((uint32_t)selq[cl[u] * k] << 2);
+      x[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] *= v[u];
+    unsigned old[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      old[u] = __hip_atomic_load(accq + cl[u] * KS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    unsigned got[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      got[u] = old[u];
+      if (ok[u]) {
+        unsigned expected = old[u];
+        __hip_atomic_compare_exchange_strong(
+            accq + cl[u] * KS, &expected, __float_as_uint(__uint_as_float(old[u]) + x[u]),
+            __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        got[u] = expected;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ok[u] && got[u] != old[u]) {
+        unsigned cur = got[u];
+        while (true) {
+          unsigned expected = cur;
+          __hip_atomic_compare_exchange_strong(
+              accq + cl[u] * KS, &expected, __float_as_uint(__uint_as_float(cur) + x[u]),
+              __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (expected == cur) break;
+          cur = expected;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  float* dst = grad_sp + (size_t)t.col0 * k;
+  for (int i = threadIdx.x; i < nsel; i += NT) {
+    const int c = i / k;
+    const float a = bacc[c * KS + (i - c * k)];
+    if (t.shared) global_add(dst + i, a);
+    else dst[i] = a;
   }
 }
 
@@ -743,7 +909,13 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
   const int B = plan->fwd_phases;
   const size_t lds = fwd_lds_bytes(R, D, plan->fwd_acc);
   const int rec_bytes = plan->fwd_rec_bytes;
-  if (k % 4 == 0 && plan->num_cols > 0) {
+  if (plan->fwd_chunk3 && plan->num_cols > 0) {
+    const int64_t items = (int64_t)plan->num_cols * ((k + 2) / 3);
+    const int grid = (int)std::min<int64_t>((items + 255) / 256, 65536);
+    hipLaunchKernelGGL(pack_cbsr3_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
+                       plan->fwd_rec, plan->num_cols, k, rec_bytes);
+    MAXK_LAUNCH_CHECK("pack_cbsr3 launch");
+  } else if (k % 4 == 0 && plan->num_cols > 0) {
     const int64_t words = (int64_t)plan->num_cols * (k + k / 4);
     const int grid = (int)std::min<int64_t>((words + 255) / 256, 65536);
     hipLaunchKernelGGL(pack_cbsr_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
@@ -778,17 +950,23 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
       case 0: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 0); break;                              \
       case 1: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 1); break;                              \
       case 2: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 2); break;                              \
-      default: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 3); break;                             \
+      case 3: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 3); break;                              \
+      case 4: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 4); break;                              \
+      case 5: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 5); break;                              \
+      case 6: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 6); break;                              \
+      default: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 7); break;                             \
     }                                                                                     \
   } while (0)
   const int W = plan->fwd_waves;
   const int FL = (plan->fwd_prefetch ? kFwdFlagPrefetch : 0) |
-                 (plan->fwd_branchless ? kFwdFlagBranchless : 0);
-  if (k % 4 == 0 && plan->fwd_acc == MAXK_ACC_F64 && plan->fwd_unroll == 8) {
+                 (plan->fwd_branchless ? kFwdFlagBranchless : 0) |
+                 (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0);
+  if ((k % 4 == 0 || plan->fwd_chunk3) && plan->fwd_acc == MAXK_ACC_F64 &&
+      plan->fwd_unroll == 8) {
     if (W == 8) FWD_LAUNCH_FL(512);
     else if (W == 6) FWD_LAUNCH_FL(384);
     else FWD_LAUNCH_FL(256);
-  } else if (k % 4 == 0) {
+  } else if (k % 4 == 0 && !plan->fwd_chunk3) {
     if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(4, MAXK_ACC_F32_CAS);
     else FWD_LAUNCH(4, MAXK_ACC_F64);
   } else {
@@ -846,6 +1024,29 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   if (plan->n_bwd_tasks == 0) return MAXK_OK;
   const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k, plan->bwd_acc);
   const dim3 grid(plan->n_bwd_tasks), block(kBwdThreads);  // general path: 512 threads
+  if (plan->bwd_rec && plan->bwd_feats == 1) {
+    const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
+    const size_t lds1 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
+                        (size_t)plan->bwd_block_cols * k;
+#define BWD1_LAUNCH(UU, NT)                                                               \
+    do {                                                                                  \
+      if (lds1 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd1_kernel<UU, NT>, lds1));     \
+      hipLaunchKernelGGL((sspmm_bwd1_kernel<UU, NT>), grid, dim3(NT), lds1, s,            \
+                         plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sp_index,     \
+                         grad_sp, k, plan->bwd_ks);                                       \
+    } while (0)
+    const int W = plan->bwd_waves, U = plan->bwd_unroll;
+    if (W == 16) BWD1_LAUNCH(16, 1024);
+    else if (W == 12) {
+      if (U >= 16) BWD1_LAUNCH(16, 768);
+      else BWD1_LAUNCH(8, 768);
+    } else if (U >= 16) BWD1_LAUNCH(16, 512);
+    else if (U >= 12) BWD1_LAUNCH(12, 512);
+    else BWD1_LAUNCH(8, 512);
+#undef BWD1_LAUNCH
+    MAXK_LAUNCH_CHECK("sspmm_bwd1 launch");
+    return MAXK_OK;
+  }
   if (plan->bwd_rec) {
     const int S = plan->bwd_slot_groups;
     const int nsel = plan->num_cols * (k / 4);

@@ -71,7 +71,8 @@ class PlanOptions(ctypes.Structure):
         ("bwd_prefetch", _i32),
         ("fwd_record_bytes", _i32),
         ("fwd_branchless", _i32),
-        ("reserved", _i32 * 2),
+        ("fwd_chunk3", _i32),
+        ("reserved", _i32 * 1),
     ]
 
 

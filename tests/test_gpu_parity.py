@@ -308,6 +308,12 @@ PLAN_OPTIONS = [
     dict(bwd_waves=12), dict(bwd_waves=16), dict(bwd_prefetch=1),
     dict(bwd_waves=12, bwd_prefetch=1), dict(bwd_waves=16, bwd_prefetch=1),
     dict(bwd_waves=12, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    # lane-chunk forward records; one-slot-per-lane packed backward
+    dict(fwd_chunk3=1), dict(fwd_chunk3=2), dict(fwd_chunk3=1, fwd_record_bytes=256),
+    dict(fwd_chunk3=1, fwd_waves=8, fwd_prefetch=1), dict(fwd_chunk3=1, fwd_branchless=2),
+    dict(bwd_features_per_lane=1, bwd_unroll=16), dict(bwd_features_per_lane=1, bwd_waves=12),
+    dict(bwd_features_per_lane=1, bwd_waves=16),
+    dict(bwd_features_per_lane=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
 ]
 
 
@@ -333,7 +339,8 @@ def test_plan_options_rejected(gpu):
     for bad in (dict(fwd_unroll=7), dict(bwd_order=3), dict(bwd_slot_groups=3),
                 dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3),
                 dict(bwd_algo=3), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
-                dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3)):
+                dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3),
+                dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 

@@ -42,13 +42,14 @@ def main():
     ap.add_argument("--dataset", default="reddit")
     ap.add_argument("--which", default="both", choices=["fwd", "bwd", "both"])
     ap.add_argument("--graph", default=None, help="N,E of a synthetic graph instead of --dataset")
+    ap.add_argument("--sigma", type=float, default=1.2, help="lognormal degree sigma")
     ap.add_argument("--fwd", default=None, help="JSON list of forward option dicts")
     ap.add_argument("--bwd", default=None, help="JSON list of backward option dicts")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = (tuple(int(x) for x in args.graph.split(",")) if args.graph
             else graphs.DATASETS[args.dataset])
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    ptr, idx = graphs.synthetic_csr(n, e, sigma=args.sigma, device=dev)
     val = graphs.sage_mean_values(ptr)
     e = idx.numel()
     h = graphs.features(n, args.dim, seed=97, device=dev)
