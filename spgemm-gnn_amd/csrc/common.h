@@ -172,6 +172,7 @@ struct maxk_plan {
   int32_t bwd_slot_groups = 1;   // S
   int32_t bwd_ks = 0;            // accumulator floats per column (k/S + 1, or k/S unpadded)
   int32_t bwd_sel_lds = 0;       // selector words of the block staged in LDS
+  int32_t bwd_cas64 = 0;         // 64-bit CAS pairs on adjacent slots (packed kernel)
   int32_t bwd_csc = 0;           // column-major kernel (sparse graphs): one wave per column
   int32_t* bwd_colptr = nullptr; // [num_cols + 1] offsets of the column-sorted records
   int64_t device_bytes = 0;

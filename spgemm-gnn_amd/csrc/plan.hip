@@ -301,6 +301,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_sel_lds >= 0 && o.bwd_sel_lds <= 2,
                  "maxk_plan_create: bwd_sel_lds must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.bwd_cas64 >= 0 && o.bwd_cas64 <= 2,
+                 "maxk_plan_create: bwd_cas64 must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_acc_pad >= 0 && o.bwd_acc_pad <= 2,
                  "maxk_plan_create: bwd_acc_pad must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_order == 0 || o.bwd_order == 1,
@@ -547,7 +549,11 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   p->bwd_slot_groups = S;
   const int nslots = k / S;
   // accumulator row stride: nslots + 1 (odd: columns start on different banks) or nslots
-  p->bwd_ks = nslots + ((packed && o.bwd_acc_pad == 2) ? 0 : 1);
+  // 64-bit CAS pairs (sspmm_bwd4_kernel<.., V>): KS even, unpadded by default
+  // (Reddit k = 16: 2.06 -> 1.78 ms; k = 8 1.24 -> 1.16; k = 32 3.21 -> 3.09)
+  p->bwd_cas64 = packed && p->bwd_feats == 4 && o.bwd_cas64 != 2;
+  if (p->bwd_cas64) p->bwd_ks = nslots + (o.bwd_acc_pad == 1 ? 4 : 0);
+  else p->bwd_ks = nslots + ((packed && o.bwd_acc_pad == 2) ? 0 : 1);
   p->bwd_sel_lds = packed && o.bwd_sel_lds != 2 ? 1 : 0;
   // bytes of LDS per column: accumulators (+ staged selector bytes, nslots per column)
   const int col_bytes = p->bwd_ks * (int)acc_bytes(p->bwd_acc) + (p->bwd_sel_lds ? nslots : 0);

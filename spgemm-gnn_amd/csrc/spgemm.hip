@@ -485,7 +485,11 @@ __global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int n, int
 // under the same LDS block). PF: the next sub-steps' records are loaded right after this
 // step's gathers are issued, so the record stream's HBM latency overlaps the LDS updates
 // (loads retire in issue order, so they must not precede the gathers the updates wait on).
-template <int U, int NT, bool PF>
+//
+// V (plan->bwd_cas64): lane q's 4 slots are stored adjacently (slot l of a column at
+// (l % L) * 4 + l / L), so its updates are 1 ds_read_b128 + 2 ds_cmpst_rtn_b64 instead of
+// 4 + 4 dword operations (KS % 4 == 0); a pair is retried if either of its floats changed.
+template <int U, int NT, bool PF, bool V>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
@@ -518,7 +522,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const __amdgpu_buffer_rsrc_t gr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
   const uint32_t* selb = (sel_lds ? sell : selg) + q;
-  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + q;
+  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + (V ? 4 * q : q);
   const uint3* rec3 = reinterpret_cast<const uint3*>(rec);
 
   // records past e1 (a padded or neighbouring record) are loaded and ignored
@@ -596,6 +600,59 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     }
     continue;
 #endif
+    if constexpr (V) {
+      using u64 = unsigned long long;
+      u64 old2[U][2];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        // one ds_read_b128 (KS % 4 == 0); a stale value only costs a CAS retry
+        const uint4 o4 = *reinterpret_cast<const uint4*>(accq + cl[u] * KS);
+        old2[u][0] = (u64)o4.x | ((u64)o4.y << 32);
+        old2[u][1] = (u64)o4.z | ((u64)o4.w << 32);
+      }
+      auto addp = [](u64 o, float a0, float a1) -> u64 {
+        const float lo = __uint_as_float((unsigned)o) + a0;
+        const float hi = __uint_as_float((unsigned)(o >> 32)) + a1;
+        return (u64)__float_as_uint(lo) | ((u64)__float_as_uint(hi) << 32);
+      };
+      u64 got2[U][2];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          got2[u][h] = old2[u][h];
+          if (ok[u]) {
+            u64 expected = old2[u][h];
+            __hip_atomic_compare_exchange_strong(a + h, &expected,
+                                                 addp(old2[u][h], x[u][2 * h], x[u][2 * h + 1]),
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            got2[u][h] = expected;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (ok[u] && got2[u][h] != old2[u][h]) {
+            u64 cur = got2[u][h];
+            while (true) {
+              u64 expected = cur;
+              __hip_atomic_compare_exchange_strong(a + h, &expected,
+                                                   addp(cur, x[u][2 * h], x[u][2 * h + 1]),
+                                                   __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (expected == cur) break;
+              cur = expected;
+            }
+          }
+        }
+      }
+      continue;
+    }
     unsigned old[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -646,7 +703,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   for (int i = threadIdx.x; i < n; i += NT) {
     const int c = i / ns;
     const int l = i - c * ns;
-    const float a = bacc[c * KS + l];
+    const float a = bacc[c * KS + (V ? (l % L) * 4 + l / L : l)];
     if (t.shared) global_add(dst + (size_t)c * k + l, a);
     else dst[(size_t)c * k + l] = a;
   }
@@ -1055,27 +1112,34 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
     const size_t lds4 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
                         (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
-#define BWD4_LAUNCH(UU, NT, PF)                                                           \
+#define BWD4_LAUNCH(UU, NT, PF, V)                                                        \
     do {                                                                                  \
-      if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, PF>, lds4)); \
-      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF>), grid, dim3(NT), lds4, s,        \
+      if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, PF, V>, lds4)); \
+      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF, V>), grid, dim3(NT), lds4, s,     \
                          plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, \
                          grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds); \
     } while (0)
     const int W = plan->bwd_waves, U = plan->bwd_unroll;
     const bool PFon = plan->bwd_prefetch != 0;
-    if (W == 16) {
-      if (PFon) BWD4_LAUNCH(6, 1024, true);
-      else BWD4_LAUNCH(6, 1024, false);
+    if (plan->bwd_cas64) {
+      if (W == 16) BWD4_LAUNCH(6, 1024, false, true);
+      else if (W == 12) BWD4_LAUNCH(8, 768, false, true);
+      else if (PFon) BWD4_LAUNCH(8, 512, true, true);
+      else if (U == 12) BWD4_LAUNCH(12, 512, false, true);
+      else if (U == 16) BWD4_LAUNCH(16, 512, false, true);
+      else BWD4_LAUNCH(8, 512, false, true);
+    } else if (W == 16) {
+      if (PFon) BWD4_LAUNCH(6, 1024, true, false);
+      else BWD4_LAUNCH(6, 1024, false, false);
     } else if (W == 12) {
-      if (PFon) BWD4_LAUNCH(8, 768, true);
-      else BWD4_LAUNCH(8, 768, false);
+      if (PFon) BWD4_LAUNCH(8, 768, true, false);
+      else BWD4_LAUNCH(8, 768, false, false);
     } else if (PFon) {
-      BWD4_LAUNCH(8, 512, true);
-    } else if (U == 16) BWD4_LAUNCH(16, 512, false);
-    else if (U == 12) BWD4_LAUNCH(12, 512, false);
-    else if (U == 4) BWD4_LAUNCH(4, 512, false);
-    else BWD4_LAUNCH(8, 512, false);
+      BWD4_LAUNCH(8, 512, true, false);
+    } else if (U == 16) BWD4_LAUNCH(16, 512, false, false);
+    else if (U == 12) BWD4_LAUNCH(12, 512, false, false);
+    else if (U == 4) BWD4_LAUNCH(4, 512, false, false);
+    else BWD4_LAUNCH(8, 512, false, false);
 #undef BWD4_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd launch");
     return MAXK_OK;

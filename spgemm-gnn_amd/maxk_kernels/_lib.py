@@ -72,7 +72,7 @@ class PlanOptions(ctypes.Structure):
         ("fwd_record_bytes", _i32),
         ("fwd_branchless", _i32),
         ("fwd_chunk3", _i32),
-        ("reserved", _i32 * 1),
+        ("bwd_cas64", _i32),
     ]
 
 
