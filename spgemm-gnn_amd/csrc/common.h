@@ -26,6 +26,7 @@ constexpr int kBwdWaves = 8;            // default wavefronts per backward work-
 constexpr int kFwdFlagPrefetch = 1;     // forward kernel flags (template FL)
 constexpr int kFwdFlagBranchless = 2;
 constexpr int kFwdFlagChunk3 = 4;
+constexpr int kFwdFlagQuad = 8;
 constexpr int kBwdTasksPerCu = 2;
 constexpr int kBwdMinTaskEdges = 16384;  // a chunk's flush costs ~as much as ~4k edges
 constexpr int kXcds = 8;
@@ -147,8 +148,7 @@ struct maxk_plan {
   int32_t bwd_prefetch = 0;
   int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per phase
   int32_t* fwd_perm = nullptr;   // CSR edge id of each permuted forward edge
-  uint32_t* fwd_cr = nullptr;    // column | (row within the task << kFwdColBits)
-  float* fwd_val = nullptr;      // val snapshot in the permuted order
+  uint2* fwd_cv = nullptr;       // {column | (row within the task << kFwdColBits), val bits}
   int32_t n_fwd_tasks = 0;
   int32_t* zero_rows = nullptr;  // rows written by split tasks (atomic), zeroed first
   int32_t n_zero_rows = 0;
@@ -173,6 +173,8 @@ struct maxk_plan {
   int32_t bwd_ks = 0;            // accumulator floats per column (k/S + 1, or k/S unpadded)
   int32_t bwd_sel_lds = 0;       // selector words of the block staged in LDS
   int32_t bwd_cas64 = 0;         // 64-bit CAS pairs on adjacent slots (packed kernel)
+  int32_t bwd_quad = 0;          // quad-shared record loads (one dword per lane + DPP)
+  int32_t fwd_quad = 0;          // quad-shared edge-word loads
   int32_t bwd_csc = 0;           // column-major kernel (sparse graphs): one wave per column
   int32_t* bwd_colptr = nullptr; // [num_cols + 1] offsets of the column-sorted records
   int64_t device_bytes = 0;

@@ -60,7 +60,7 @@ __global__ void fwd_key_kernel(const int32_t* __restrict__ idx, const int32_t* _
 // off[t * (B + 1) + b] = first edge of task t whose column is >= b * NC / B (the task's
 // edges are column-sorted).
 __global__ void fwd_phase_kernel(const FwdTask* __restrict__ tasks, int ntasks,
-                                 const uint32_t* __restrict__ cr, int NC, int B,
+                                 const uint2* __restrict__ cv, int NC, int B,
                                  int32_t* __restrict__ off) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ntasks * (B + 1)) return;
@@ -72,7 +72,7 @@ __global__ void fwd_phase_kernel(const FwdTask* __restrict__ tasks, int ntasks,
   if (b == 0) { off[i] = lo; return; }
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if ((cr[mid] & kFwdColMask) < bound) lo = mid + 1; else hi = mid;
+    if ((cv[mid].x & kFwdColMask) < bound) lo = mid + 1; else hi = mid;
   }
   off[i] = lo;
 }
@@ -81,12 +81,13 @@ __global__ void gather_fwd_kernel(const int32_t* __restrict__ perm,
                                   const int32_t* __restrict__ idx,
                                   const int32_t* __restrict__ rl_of,
                                   const float* __restrict__ val, int64_t E,
-                                  uint32_t* __restrict__ cr, float* __restrict__ fval) {
+                                  uint2* __restrict__ cv, bool with_cr) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < E;
        j += (int64_t)gridDim.x * blockDim.x) {
     const int32_t e = perm[j];
-    if (cr) cr[j] = (uint32_t)idx[e] | ((uint32_t)rl_of[e] << kFwdColBits);
-    fval[j] = val ? val[e] : 1.0f;
+    // one 8-B edge word {column | row-in-tile << kFwdColBits, val}: a single load per edge
+    if (with_cr) cv[j].x = (uint32_t)idx[e] | ((uint32_t)rl_of[e] << kFwdColBits);
+    cv[j].y = __float_as_uint(val ? val[e] : 1.0f);
   }
 }
 
@@ -184,8 +185,7 @@ static void free_plan(maxk_plan* p) {
   dfree(p->fwd_tasks);
   dfree(p->fwd_rec);
   dfree(p->fwd_perm);
-  dfree(p->fwd_cr);
-  dfree(p->fwd_val);
+  dfree(p->fwd_cv);
   dfree(p->fwd_phase_off);
   dfree(p->zero_rows);
   dfree(p->bwd_tasks);
@@ -301,6 +301,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_sel_lds >= 0 && o.bwd_sel_lds <= 2,
                  "maxk_plan_create: bwd_sel_lds must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.quad_loads >= 0 && o.quad_loads <= 2,
+                 "maxk_plan_create: quad_loads must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_cas64 >= 0 && o.bwd_cas64 <= 2,
                  "maxk_plan_create: bwd_cas64 must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_acc_pad >= 0 && o.bwd_acc_pad <= 2,
@@ -458,10 +460,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       FWD_TRY(hipMalloc(&d_tmp, tb));
       FWD_TRY(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_kin, d_kout, d_ids, p->fwd_perm,
                                                  (int)E, 0, cbits + tbits, s));
-      FWD_TRY(hipMalloc(&p->fwd_cr, sizeof(uint32_t) * E));
-      FWD_TRY(hipMalloc(&p->fwd_val, sizeof(float) * E));
+      FWD_TRY(hipMalloc(&p->fwd_cv, sizeof(uint2) * E));
       hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->fwd_perm,
-                         idx, d_rl, val, E, p->fwd_cr, p->fwd_val);
+                         idx, d_rl, val, E, p->fwd_cv, true);
       FWD_TRY(hipGetLastError());
       FWD_TRY(hipStreamSynchronize(s));
       fwd_cleanup();
@@ -491,7 +492,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     PLAN_TRY(hipMalloc(&p->fwd_phase_off, sizeof(int32_t) * nt * (B + 1)));
     p->device_bytes += sizeof(int32_t) * nt * (B + 1);
     hipLaunchKernelGGL(fwd_phase_kernel, dim3((nt * (B + 1) + 255) / 256), dim3(256), 0, s,
-                       p->fwd_tasks, nt, p->fwd_cr, NC, B, p->fwd_phase_off);
+                       p->fwd_tasks, nt, p->fwd_cv, NC, B, p->fwd_phase_off);
     PLAN_TRY(hipGetLastError());
   }
   if (!zrows.empty()) {
@@ -552,6 +553,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // 64-bit CAS pairs (sspmm_bwd4_kernel<.., V>): KS even, unpadded by default
   // (Reddit k = 16: 2.06 -> 1.78 ms; k = 8 1.24 -> 1.16; k = 32 3.21 -> 3.09)
   p->bwd_cas64 = packed && p->bwd_feats == 4 && o.bwd_cas64 != 2;
+  // (Reddit bwd k = 16 1.76 -> 1.70 ms, k = 32 3.08 -> 2.93, k = 64 5.43 -> 4.86; the forward's
+  // 8-B edge words gain nothing: forward only on request)
+  p->bwd_quad = o.quad_loads != 2;
+  p->fwd_quad = o.quad_loads == 1;
   if (p->bwd_cas64) p->bwd_ks = nslots + (o.bwd_acc_pad == 1 ? 4 : 0);
   else p->bwd_ks = nslots + ((packed && o.bwd_acc_pad == 2) ? 0 : 1);
   p->bwd_sel_lds = packed && o.bwd_sel_lds != 2 ? 1 : 0;
@@ -785,7 +790,7 @@ extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* st
   if (p->fwd_perm)
     hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
                        (hipStream_t)stream, p->fwd_perm, nullptr, nullptr, val, p->num_edges,
-                       nullptr, p->fwd_val);
+                       p->fwd_cv, false);
   MAXK_LAUNCH_CHECK("maxk_plan_refresh_values launch");
   return MAXK_OK;
 }

@@ -33,6 +33,16 @@ namespace maxk {
 template <int ACC>
 struct LdsAcc;
 
+// Quad-shared loads: the L lanes of an edge (L % 4 == 0, quad-aligned) need the same edge
+// record; each lane loads ONE dword of it and quad_perm DPP moves broadcast the words, so
+// the texture path returns 4 B per lane instead of the whole record per lane (PMC: TD busy
+// ~93 % in both kernels, the record/edge-word loads were a third of its bytes).
+template <int W>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+  static_assert(W >= 0 && W < 4, "quad lane");
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, W * 0x55, 0xf, 0xf, false);
+}
+
 // MAXK_PROBE (tools/ builds only, `make probe`; never in the product library): speed probes
 // with wrong numerics. 1: forward ds_add_u64 of the f64 bits; 2: forward without LDS
 // updates; 3: backward ds_add_u32 of the f32 bits instead of the read + CAS; 4: backward
@@ -135,25 +145,34 @@ __global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
 template <int U, class A, int FL>
 __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, int wave,
                                            int nwaves, int EPS, int slot, int l0, bool lane_on,
-                                           const uint32_t* __restrict__ cr,
-                                           const float* __restrict__ fval,
+                                           const uint2* __restrict__ cv,
                                            const uint8_t* __restrict__ rec, int rec_bytes,
                                            int D, int k) {
   using T = typename A::T;
   constexpr bool PF = (FL & kFwdFlagPrefetch) != 0;
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
+  constexpr bool QL = (FL & kFwdFlagQuad) != 0;  // L % 4 == 0: lanes load one word each
   const int last = e1 - 1;
+  const uint32_t* cvw = reinterpret_cast<const uint32_t*>(cv) + (threadIdx.x & 1);
+  auto load_cv = [&](int e) -> uint2 {
+    if constexpr (QL) return make_uint2(cvw[2 * (size_t)e], 0u);
+    else return cv[e];
+  };
+  auto split_cv = [&](uint2 w, uint32_t& c, float& v) {
+    if constexpr (QL) {
+      c = quad_bcast<0>(w.x);
+      v = __uint_as_float(quad_bcast<1>(w.x));
+    } else {
+      c = w.x;
+      v = __uint_as_float(w.y);
+    }
+  };
   const int stride = nwaves * EPS * U;
   int base = e0 + wave * EPS * U;
-  uint32_t cn[U];
-  float vn[U];
+  uint2 wn[U];
   if (PF) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = min(base + u * EPS + slot, last);
-      cn[u] = cr[e];
-      vn[u] = fval[e];
-    }
+    for (int u = 0; u < U; ++u) wn[u] = load_cv(min(base + u * EPS + slot, last));
   }
   for (; base < e1; base += stride) {
     uint32_t cw[U];
@@ -163,14 +182,7 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
     for (int u = 0; u < U; ++u) {
       const int e = base + u * EPS + slot;
       ok[u] = lane_on && e < e1;
-      if (PF) {
-        cw[u] = cn[u];
-        v[u] = vn[u];
-      } else {
-        const int ec = ok[u] ? e : last;
-        cw[u] = cr[ec];
-        v[u] = fval[ec];
-      }
+      split_cv(PF ? wn[u] : load_cv(ok[u] ? e : last), cw[u], v[u]);
     }
     float4 x[U];
     uint32_t sel[U];
@@ -189,11 +201,7 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
     if (PF) {  // unconditional (clamped), see sspmm_bwd4_kernel
       __builtin_amdgcn_sched_barrier(0);  // keep every gather ahead of these loads
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = min(base + stride + u * EPS + slot, last);
-        cn[u] = cr[e];
-        vn[u] = fval[e];
-      }
+      for (int u = 0; u < U; ++u) wn[u] = load_cv(min(base + stride + u * EPS + slot, last));
       __builtin_amdgcn_sched_barrier(0);
     }
     // Branchless: idle lanes add 0 at their clamped (valid) edge's addresses; with a branch
@@ -228,7 +236,7 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
 template <int VEC, int ACC, int U, int NT, int FL>
 __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     const FwdTask* __restrict__ tasks, int ntasks, const int32_t* __restrict__ phase_off,
-    int phases, int phase, const uint32_t* __restrict__ cr, const float* __restrict__ fval,
+    int phases, int phase, const uint2* __restrict__ cv,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
     const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
     int tile_rows, int rot_ticks) {
@@ -290,20 +298,21 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     // memory-level parallelism comes from U independent sub-steps per wave. Out-of-range
     // lanes load a clamped (valid) edge and skip the update.
     if (emid >= 0) {
-      fwd_edges4<U, A, FL>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+      fwd_edges4<U, A, FL>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, D, k);
-      fwd_edges4<U, A, FL>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+      fwd_edges4<U, A, FL>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, D, k);
     } else {
-      fwd_edges4<U, A, FL>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cr, fval, rec,
+      fwd_edges4<U, A, FL>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, D, k);
     }
   } else {
     for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
       const int e = base + slot;
       if (lane_on && e < t.e1) {
-        const uint32_t cwv = cr[e];
-        const float v = fval[e];
+        const uint2 w = cv[e];
+        const uint32_t cwv = w.x;
+        const float v = __uint_as_float(w.y);
         T* arow = acc + (cwv >> kFwdColBits) * D;
         const size_t rb = (size_t)(cwv & kFwdColMask) * k;
         for (int l = l0; l < k; l += L) A::add(arow + sp_index[rb + l], v * sp_data[rb + l]);
@@ -489,7 +498,7 @@ __global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int n, int
 // V (plan->bwd_cas64): lane q's 4 slots are stored adjacently (slot l of a column at
 // (l % L) * 4 + l / L), so its updates are 1 ds_read_b128 + 2 ds_cmpst_rtn_b64 instead of
 // 4 + 4 dword operations (KS % 4 == 0); a pair is retried if either of its floats changed.
-template <int U, int NT, bool PF, bool V>
+template <int U, int NT, bool PF, bool V, bool Q>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
@@ -527,10 +536,16 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
 
   // records past e1 (a padded or neighbouring record) are loaded and ignored
   int base = t.e0 + wave * EPS * U;
+  // Q: lane loads dword min(q & 3, 2) of its edge's record (quad_bcast below)
+  const uint32_t* recw = rec + min(lane & 3, 2);
+  auto load_rec = [&](int e) -> uint3 {
+    if constexpr (Q) return make_uint3(recw[3 * (size_t)e], 0u, 0u);
+    else return rec3[e];
+  };
   uint3 rn[U];
   if (PF) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) rn[u] = rec3[min(base + u * EPS + slot, t.e1 - 1)];
+    for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + u * EPS + slot, t.e1 - 1));
   }
   for (; base < t.e1; base += stride) {
     uint32_t go[U], cl[U];
@@ -540,10 +555,16 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     for (int u = 0; u < U; ++u) {
       const int e = base + u * EPS + slot;
       ok[u] = lane_on && e < t.e1;
-      const uint3 r3 = PF ? rn[u] : rec3[e];
-      go[u] = r3.x;
-      cl[u] = r3.y;
-      v[u] = __uint_as_float(r3.z);
+      const uint3 r3 = PF ? rn[u] : load_rec(e);
+      if constexpr (Q) {
+        go[u] = quad_bcast<0>(r3.x);
+        cl[u] = quad_bcast<1>(r3.x);
+        v[u] = __uint_as_float(quad_bcast<2>(r3.x));
+      } else {
+        go[u] = r3.x;
+        cl[u] = r3.y;
+        v[u] = __uint_as_float(r3.z);
+      }
     }
     uint32_t s[U];
 #pragma unroll
@@ -565,7 +586,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
                // for these loads too (vmcnt counts both paths)
       __builtin_amdgcn_sched_barrier(0);  // keep every gather ahead of these loads
 #pragma unroll
-      for (int u = 0; u < U; ++u) rn[u] = rec3[min(base + stride + u * EPS + slot, t.e1 - 1)];
+      for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + stride + u * EPS + slot, t.e1 - 1));
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
@@ -993,7 +1014,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
     for (int b = 0; b < (rot ? 1 : B); ++b)                                               \
       hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU, NT, FL>), dim3(g), dim3(NT), lds, s, \
                          plan->fwd_tasks, plan->n_fwd_tasks, plan->fwd_phase_off, B, b,   \
-                         plan->fwd_cr, plan->fwd_val, sp_data, sp_index, plan->fwd_rec,   \
+                         plan->fwd_cv, sp_data, sp_index, plan->fwd_rec,                  \
                          rec_bytes, out, D, k, R, rot);                                   \
   } while (0)
 #define FWD_LAUNCH(V, A)                                                                  \
@@ -1003,7 +1024,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
   } while (0)
 #define FWD_LAUNCH_FL(NT)                                                                 \
   do {                                                                                    \
-    switch (FL) {                                                                         \
+    switch (FL & 7) {                                                                     \
       case 0: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 0); break;                              \
       case 1: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 1); break;                              \
       case 2: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 2); break;                              \
@@ -1014,13 +1035,29 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
       default: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 7); break;                             \
     }                                                                                     \
   } while (0)
+#define FWD_LAUNCH_FLQ()                                                                  \
+  do {                                                                                    \
+    switch (FL & 7) {                                                                     \
+      case 0: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 8); break;                             \
+      case 1: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 9); break;                             \
+      case 2: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 10); break;                            \
+      case 3: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 11); break;                            \
+      case 4: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 12); break;                            \
+      case 5: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 13); break;                            \
+      case 6: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 14); break;                            \
+      default: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 15); break;                           \
+    }                                                                                     \
+  } while (0)
   const int W = plan->fwd_waves;
+  const int Lf = plan->fwd_chunk3 ? (k + 2) / 3 : k / 4;  // lanes per edge
   const int FL = (plan->fwd_prefetch ? kFwdFlagPrefetch : 0) |
                  (plan->fwd_branchless ? kFwdFlagBranchless : 0) |
-                 (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0);
+                 (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0) |
+                 (plan->fwd_quad && Lf % 4 == 0 && W == 4 ? kFwdFlagQuad : 0);
   if ((k % 4 == 0 || plan->fwd_chunk3) && plan->fwd_acc == MAXK_ACC_F64 &&
       plan->fwd_unroll == 8) {
-    if (W == 8) FWD_LAUNCH_FL(512);
+    if (FL & kFwdFlagQuad) FWD_LAUNCH_FLQ();
+    else if (W == 8) FWD_LAUNCH_FL(512);
     else if (W == 6) FWD_LAUNCH_FL(384);
     else FWD_LAUNCH_FL(256);
   } else if (k % 4 == 0 && !plan->fwd_chunk3) {
@@ -1031,6 +1068,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
     else FWD_LAUNCH(1, MAXK_ACC_F64);
   }
 #undef FWD_LAUNCH_FL
+#undef FWD_LAUNCH_FLQ
 #undef FWD_LAUNCH
 #undef FWD_LAUNCH1
   MAXK_LAUNCH_CHECK("spgemm_fwd launch");
@@ -1112,34 +1150,47 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
     const size_t lds4 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
                         (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
-#define BWD4_LAUNCH(UU, NT, PF, V)                                                        \
+#define BWD4_LAUNCH(UU, NT, PF, V, Q)                                                     \
     do {                                                                                  \
-      if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, PF, V>, lds4)); \
-      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF, V>), grid, dim3(NT), lds4, s,     \
+      if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, PF, V, Q>, lds4)); \
+      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF, V, Q>), grid, dim3(NT), lds4, s,  \
                          plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, \
                          grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds); \
     } while (0)
     const int W = plan->bwd_waves, U = plan->bwd_unroll;
     const bool PFon = plan->bwd_prefetch != 0;
+    const bool QL = plan->bwd_quad && (k / S / 4) % 4 == 0;  // quad-aligned edge lane groups
     if (plan->bwd_cas64) {
-      if (W == 16) BWD4_LAUNCH(6, 1024, false, true);
-      else if (W == 12) BWD4_LAUNCH(8, 768, false, true);
-      else if (PFon) BWD4_LAUNCH(8, 512, true, true);
-      else if (U == 12) BWD4_LAUNCH(12, 512, false, true);
-      else if (U == 16) BWD4_LAUNCH(16, 512, false, true);
-      else BWD4_LAUNCH(8, 512, false, true);
+      if (W == 16) {
+        if (QL) BWD4_LAUNCH(6, 1024, false, true, true);
+        else BWD4_LAUNCH(6, 1024, false, true, false);
+      } else if (W == 12) {
+        if (QL) BWD4_LAUNCH(8, 768, false, true, true);
+        else BWD4_LAUNCH(8, 768, false, true, false);
+      } else if (PFon) {
+        if (QL) BWD4_LAUNCH(8, 512, true, true, true);
+        else BWD4_LAUNCH(8, 512, true, true, false);
+      } else if (U == 12) {
+        if (QL) BWD4_LAUNCH(12, 512, false, true, true);
+        else BWD4_LAUNCH(12, 512, false, true, false);
+      } else if (U == 16) {
+        BWD4_LAUNCH(16, 512, false, true, false);
+      } else {
+        if (QL) BWD4_LAUNCH(8, 512, false, true, true);
+        else BWD4_LAUNCH(8, 512, false, true, false);
+      }
     } else if (W == 16) {
-      if (PFon) BWD4_LAUNCH(6, 1024, true, false);
-      else BWD4_LAUNCH(6, 1024, false, false);
+      if (PFon) BWD4_LAUNCH(6, 1024, true, false, false);
+      else BWD4_LAUNCH(6, 1024, false, false, false);
     } else if (W == 12) {
-      if (PFon) BWD4_LAUNCH(8, 768, true, false);
-      else BWD4_LAUNCH(8, 768, false, false);
+      if (PFon) BWD4_LAUNCH(8, 768, true, false, false);
+      else BWD4_LAUNCH(8, 768, false, false, false);
     } else if (PFon) {
-      BWD4_LAUNCH(8, 512, true, false);
-    } else if (U == 16) BWD4_LAUNCH(16, 512, false, false);
-    else if (U == 12) BWD4_LAUNCH(12, 512, false, false);
-    else if (U == 4) BWD4_LAUNCH(4, 512, false, false);
-    else BWD4_LAUNCH(8, 512, false, false);
+      BWD4_LAUNCH(8, 512, true, false, false);
+    } else if (U == 16) BWD4_LAUNCH(16, 512, false, false, false);
+    else if (U == 12) BWD4_LAUNCH(12, 512, false, false, false);
+    else if (U == 4) BWD4_LAUNCH(4, 512, false, false, false);
+    else BWD4_LAUNCH(8, 512, false, false, false);
 #undef BWD4_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd launch");
     return MAXK_OK;

@@ -73,6 +73,8 @@ class PlanOptions(ctypes.Structure):
         ("fwd_branchless", _i32),
         ("fwd_chunk3", _i32),
         ("bwd_cas64", _i32),
+        ("quad_loads", _i32),
+        ("reserved2", _i32 * 3),
     ]
 
 

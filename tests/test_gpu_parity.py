@@ -318,6 +318,9 @@ PLAN_OPTIONS = [
     dict(bwd_cas64=2), dict(bwd_acc_pad=1), dict(bwd_unroll=12), dict(bwd_unroll=16),
     dict(bwd_cas64=2, bwd_waves=12), dict(bwd_cas64=2, bwd_prefetch=1),
     dict(bwd_slot_groups=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_acc_pad=1),
+    # quad-shared record loads: off, forward too, with prefetch / more waves / unroll 12
+    dict(quad_loads=2), dict(quad_loads=1), dict(quad_loads=1, fwd_prefetch=1),
+    dict(quad_loads=1, fwd_chunk3=1), dict(bwd_prefetch=1, bwd_waves=16),
 ]
 
 
@@ -344,7 +347,7 @@ def test_plan_options_rejected(gpu):
                 dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3),
                 dict(bwd_algo=3), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
                 dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3),
-                dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3)):
+                dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 
