@@ -175,6 +175,7 @@ struct maxk_plan {
   int32_t bwd_cas64 = 0;         // 64-bit CAS pairs on adjacent slots (packed kernel)
   int32_t bwd_quad = 0;          // quad-shared record loads (one dword per lane + DPP)
   int32_t fwd_quad = 0;          // quad-shared edge-word loads
+  int32_t fwd_two_tables = 0;    // gather from sp_data / sp_index directly (no pack)
   int32_t bwd_csc = 0;           // column-major kernel (sparse graphs): one wave per column
   int32_t* bwd_colptr = nullptr; // [num_cols + 1] offsets of the column-sorted records
   int64_t device_bytes = 0;

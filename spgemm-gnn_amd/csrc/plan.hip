@@ -557,6 +557,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // 8-B edge words gain nothing: forward only on request)
   p->bwd_quad = o.quad_loads != 2;
   p->fwd_quad = o.quad_loads == 1;
+  MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
+                 "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
+  // (Reddit k = 32: 2.65 -> 2.53 ms, k = 64: 4.98 -> 4.92; k = 16: 1.35 vs 1.39 packed)
+  p->fwd_two_tables = o.fwd_two_tables == 1 || (o.fwd_two_tables == 0 && k >= 32);
   if (p->bwd_cas64) p->bwd_ks = nslots + (o.bwd_acc_pad == 1 ? 4 : 0);
   else p->bwd_ks = nslots + ((packed && o.bwd_acc_pad == 2) ? 0 : 1);
   p->bwd_sel_lds = packed && o.bwd_sel_lds != 2 ? 1 : 0;

@@ -147,7 +147,7 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
                                            int nwaves, int EPS, int slot, int l0, bool lane_on,
                                            const uint2* __restrict__ cv,
                                            const uint8_t* __restrict__ rec, int rec_bytes,
-                                           int D, int k) {
+                                           const uint8_t* __restrict__ seltab, int D, int k) {
   using T = typename A::T;
   constexpr bool PF = (FL & kFwdFlagPrefetch) != 0;
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
@@ -195,7 +195,11 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
         sel[u] = w.w;
       } else {
         x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
-        sel[u] = *reinterpret_cast<const uint32_t*>(rp + 4 * k + l0);
+        // two tables (plan->fwd_two_tables): values straight from sp_data, selectors from
+        // sp_index (no per-call pack); else the selector word of the packed record
+        const uint8_t* sp = seltab ? seltab + (size_t)(cw[u] & kFwdColMask) * k + l0
+                                   : rp + 4 * k + l0;
+        sel[u] = *reinterpret_cast<const uint32_t*>(sp);
       }
     }
     if (PF) {  // unconditional (clamped), see sspmm_bwd4_kernel
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     int phases, int phase, const uint2* __restrict__ cv,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
     const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
-    int tile_rows, int rot_ticks) {
+    int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab) {
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
@@ -299,12 +303,12 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     // lanes load a clamped (valid) edge and skip the update.
     if (emid >= 0) {
       fwd_edges4<U, A, FL>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, D, k);
+                           rec_bytes, seltab, D, k);
       fwd_edges4<U, A, FL>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, D, k);
+                           rec_bytes, seltab, D, k);
     } else {
       fwd_edges4<U, A, FL>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, D, k);
+                           rec_bytes, seltab, D, k);
     }
   } else {
     for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
@@ -987,7 +991,14 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
   const int B = plan->fwd_phases;
   const size_t lds = fwd_lds_bytes(R, D, plan->fwd_acc);
   const int rec_bytes = plan->fwd_rec_bytes;
-  if (plan->fwd_chunk3 && plan->num_cols > 0) {
+  // two tables: values read straight from sp_data (4k-byte rows), selectors from sp_index
+  const bool two = plan->fwd_two_tables && !plan->fwd_chunk3 && k % 4 == 0;
+  const uint8_t* seltab = two ? sp_index : nullptr;
+  const uint8_t* recp = two ? reinterpret_cast<const uint8_t*>(sp_data) : plan->fwd_rec;
+  const int rec_bytes_eff = two ? 4 * k : rec_bytes;
+  if (two) {
+    // nothing to pack
+  } else if (plan->fwd_chunk3 && plan->num_cols > 0) {
     const int64_t items = (int64_t)plan->num_cols * ((k + 2) / 3);
     const int grid = (int)std::min<int64_t>((items + 255) / 256, 65536);
     hipLaunchKernelGGL(pack_cbsr3_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
@@ -1014,8 +1025,8 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
     for (int b = 0; b < (rot ? 1 : B); ++b)                                               \
       hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU, NT, FL>), dim3(g), dim3(NT), lds, s, \
                          plan->fwd_tasks, plan->n_fwd_tasks, plan->fwd_phase_off, B, b,   \
-                         plan->fwd_cv, sp_data, sp_index, plan->fwd_rec,                  \
-                         rec_bytes, out, D, k, R, rot);                                   \
+                         plan->fwd_cv, sp_data, sp_index, recp,                           \
+                         rec_bytes_eff, out, D, k, R, rot, seltab);                       \
   } while (0)
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \

@@ -74,7 +74,8 @@ class PlanOptions(ctypes.Structure):
         ("fwd_chunk3", _i32),
         ("bwd_cas64", _i32),
         ("quad_loads", _i32),
-        ("reserved2", _i32 * 3),
+        ("fwd_two_tables", _i32),
+        ("reserved2", _i32 * 2),
     ]
 
 

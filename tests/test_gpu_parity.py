@@ -321,6 +321,7 @@ PLAN_OPTIONS = [
     # quad-shared record loads: off, forward too, with prefetch / more waves / unroll 12
     dict(quad_loads=2), dict(quad_loads=1), dict(quad_loads=1, fwd_prefetch=1),
     dict(quad_loads=1, fwd_chunk3=1), dict(bwd_prefetch=1, bwd_waves=16),
+    dict(fwd_two_tables=1), dict(fwd_two_tables=2), dict(fwd_two_tables=1, fwd_prefetch=1),
 ]
 
 
@@ -347,7 +348,7 @@ def test_plan_options_rejected(gpu):
                 dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3),
                 dict(bwd_algo=3), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
                 dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3),
-                dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3)):
+                dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3), dict(fwd_two_tables=3)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 
