@@ -28,7 +28,7 @@ constexpr int kFwdFlagBranchless = 2;
 constexpr int kFwdFlagChunk3 = 4;
 constexpr int kFwdFlagQuad = 8;
 constexpr int kBwdTasksPerCu = 2;
-constexpr int kBwdMinTaskEdges = 16384;  // a chunk's flush costs ~as much as ~4k edges
+constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k atomics) vs its edges
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
 constexpr double kFwdSlotEdgeRate = 1.5e8;  // edges/s one forward work-group slot sustains

@@ -667,8 +667,13 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     // every chunk task flushes its whole block (C * k atomics) however few edges it has:
     // keep >= kBwdMinTaskEdges edges per task (a row shard of a multi-GPU partition has
     // 1/W of the edges over the same blocks)
-    const int nch = (int)std::max<int64_t>(
-        1, std::min<int64_t>(chunks, E / ((int64_t)nblocks * min_task_edges)));
+    // ... but not fewer tasks than CUs while those keep >= 16k edges (a row shard of an
+    // 8-GPU partition: 256 tasks of ~56k edges ran 0.24 ms, 512 of ~28k 0.27, 128 0.40)
+    int64_t nch64 = std::min<int64_t>(chunks, E / ((int64_t)nblocks * min_task_edges));
+    const int64_t fl = ((int64_t)cus + (int64_t)nblocks * S - 1) / ((int64_t)nblocks * S);
+    if (o.bwd_min_task_edges == 0 && nch64 < fl && E / ((int64_t)nblocks * fl) >= 16384)
+      nch64 = std::min<int64_t>(chunks, fl);
+    const int nch = (int)std::max<int64_t>(1, nch64);
     std::vector<int32_t> rb(nch + 1);
     for (int j = 0; j <= nch; ++j) {
       const int64_t target = E * j / nch;

@@ -7,14 +7,16 @@ exchange per direction:
 * partition: contiguous row ranges balanced by nnz; rank q owns rows [start_q, end_q),
   their CSR slice (columns keep pointing at any node) and computes the top-k of its own
   rows (weights are replicated);
-* forward : one RCCL all-gather of the k-sparse CBSR block (sp_data f32 + sp_index u8 as
-  5k bytes per node) into a table padded to W x max_rows rows, then the local SpGEMM over
-  the rank's rows with a rectangular plan whose column ids are remapped into that
-  padded table (remapping is done once, at partition time);
+* forward : RCCL all-gathers of the k-sparse CBSR block (sp_data f32 and sp_index u8,
+  coalesced into one group call) straight into the tables the kernels read, padded to
+  W x max_rows rows; the rank's top-k can be written directly into its send buffers
+  (``local_buffers``), so the exchange moves no extra copies. Then the local SpGEMM over
+  the rank's rows with a rectangular plan whose column ids are remapped into that padded
+  table (remapping is done once, at partition time);
 * backward: the local SSpMM produces a partial grad_sp for every (padded) column; an
   RCCL reduce-scatter (sum) returns each rank its own rows' gradient.
 
-Bytes exchanged per step are 5kN (all-gather) + 4kN (reduce-scatter), i.e. 18.6 MB +
+Bytes exchanged per step are 5kN (all-gathers) + 4kN (reduce-scatter), i.e. 18.6 MB +
 14.9 MB for Reddit at k=16, against 238 MB for all-gathering dense features.
 """
 from __future__ import annotations
@@ -88,10 +90,9 @@ class ShardedAggregation:
         self.ptr, self.idx, self.val = part.local_csr(ptr, idx, val, rank)
         dev = self.ptr.device
         m, k = part.max_rows, self.dim_k
-        # one collective per step: each CBSR row travels as 5k bytes {k f32 values, k u8
-        # selectors}, split into the two tables after the all-gather
-        self.send = torch.zeros((m, 5 * k), dtype=torch.uint8, device=dev)
-        self.table_bytes = torch.empty((part.padded_rows, 5 * k), dtype=torch.uint8, device=dev)
+        # padded send buffers (rows >= n_local stay zero) and the all-gathered tables
+        self.send_data = torch.zeros((m, k), dtype=torch.float32, device=dev)
+        self.send_index = torch.zeros((m, k), dtype=torch.uint8, device=dev)
         self.table_data = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
         self.table_index = torch.empty((part.padded_rows, k), dtype=torch.uint8, device=dev)
         self.grad_local = torch.empty((m, k), dtype=torch.float32, device=dev)
@@ -103,14 +104,26 @@ class ShardedAggregation:
         self._fwd = fwd or (lambda d, i: self.plan.forward(d, i))
         self._bwd = bwd or (lambda g, i: self.plan.backward(g, i))
 
+    def local_buffers(self):
+        """(sp_data, sp_index) views [n_local, k] of the send buffers: write this rank's
+        top-k here (``maxk_forward(h, k, out=...)``) and ``gather`` sends them as they are."""
+        return self.send_data[: self.n_local], self.send_index[: self.n_local]
+
     def gather(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> None:
-        """All-gather this rank's CBSR rows into the padded table (RCCL over xGMI)."""
-        n, k = self.n_local, self.dim_k
-        self.send[:n, :4 * k].copy_(sp_data_local.contiguous().view(torch.uint8))
-        self.send[:n, 4 * k:].copy_(sp_index_local)
-        dist.all_gather_into_tensor(self.table_bytes, self.send, group=self.group)
-        self.table_data.view(torch.uint8).view(-1, 4 * k).copy_(self.table_bytes[:, :4 * k])
-        self.table_index.copy_(self.table_bytes[:, 4 * k:])
+        """All-gather this rank's CBSR rows into the padded tables (RCCL over xGMI)."""
+        n = self.n_local
+        if sp_data_local.data_ptr() != self.send_data.data_ptr():
+            self.send_data[:n].copy_(sp_data_local)
+        if sp_index_local.data_ptr() != self.send_index.data_ptr():
+            self.send_index[:n].copy_(sp_index_local)
+        cm = getattr(dist, "_coalescing_manager", None)
+        if cm is not None and self.table_data.is_cuda:
+            with cm(group=self.group, device=self.table_data.device):
+                dist.all_gather_into_tensor(self.table_data, self.send_data, group=self.group)
+                dist.all_gather_into_tensor(self.table_index, self.send_index, group=self.group)
+        else:
+            dist.all_gather_into_tensor(self.table_data, self.send_data, group=self.group)
+            dist.all_gather_into_tensor(self.table_index, self.send_index, group=self.group)
 
     def forward(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> torch.Tensor:
         self.gather(sp_data_local, sp_index_local)

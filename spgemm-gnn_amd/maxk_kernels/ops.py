@@ -53,7 +53,7 @@ def _check_tensor(t: torch.Tensor, name: str, dtype: Optional[torch.dtype] = Non
 # MaxK top-k
 # -------------------------------------------------------------------------------------
 def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
-                 return_index: bool = False):
+                 return_index: bool = False, out=None):
     """MaxK nonlinearity -> CBSR. Reference: ``maxk_forward(input, k) -> [N, k] f32``.
 
     Checks (bindings.cpp:27-30): "input must be a CUDA tensor", "input must be
@@ -61,6 +61,8 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
     ``mode='exact'`` selects the true top-k (utils/models.py:14 semantics), ``'ref_compat'``
     the reference kernel's 8-step bisection, bit-exact. With ``return_index=True`` returns
     ``(sp_data, sp_index)`` with ``sp_index`` u8 ``[N, k]`` in ascending feature order.
+    ``out=(sp_data, sp_index)`` writes into caller-owned contiguous ``[N, k]`` tensors (e.g.
+    the send buffers of :class:`maxk_kernels.dist.ShardedAggregation`).
     """
     _need(input.is_cuda, "input must be a CUDA tensor")
     _need(input.is_contiguous(), "input must be contiguous")
@@ -70,8 +72,17 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
     _need(d <= 256, "input dimension must be <= 256 (u8 selectors)")
     _need(input.dtype == torch.float32, "input must be float32")
     _need(mode in TOPK_MODES, f"mode must be one of {sorted(TOPK_MODES)}")
-    sp_data = torch.empty((n, k), dtype=torch.float32, device=input.device)
-    sp_index = torch.empty((n, k), dtype=torch.uint8, device=input.device)
+    if out is None:
+        sp_data = torch.empty((n, k), dtype=torch.float32, device=input.device)
+        sp_index = torch.empty((n, k), dtype=torch.uint8, device=input.device)
+    else:
+        sp_data, sp_index = out
+        _need(sp_data.shape == (n, k) and sp_data.dtype == torch.float32 and
+              sp_data.is_contiguous() and sp_data.device == input.device,
+              "out[0] must be a contiguous float32 [N, k] tensor on the input's device")
+        _need(sp_index.shape == (n, k) and sp_index.dtype == torch.uint8 and
+              sp_index.is_contiguous() and sp_index.device == input.device,
+              "out[1] must be a contiguous uint8 [N, k] tensor on the input's device")
     with torch.cuda.device(input.device):
         check(lib.maxk_topk_cbsr(_p(input), _p(sp_data), _p(sp_index), n, d, k,
                                  TOPK_MODES[mode], _stream()), "maxk_forward")

@@ -92,5 +92,15 @@ def test_sharded_aggregation_rccl_world1(gpu):
         torch.cuda.synchronize()
         assert torch.allclose(y, y_ref, rtol=1e-5, atol=1e-6)
         assert torch.allclose(gs, gs_ref, rtol=1e-5, atol=1e-6)
+        # top-k written straight into the send buffers (bench.py's N > 1 step): no copies
+        sdb, sib = shard.local_buffers()
+        r = mk.maxk_forward(x, k, return_index=True, out=(sdb, sib))
+        assert r[0] is sdb and r[1] is sib
+        assert torch.equal(sdb, sd) and torch.equal(sib, si)
+        y2 = shard.forward(sdb, sib)
+        torch.cuda.synchronize()
+        assert torch.allclose(y2, y_ref, rtol=1e-5, atol=1e-6)
+        with pytest.raises(RuntimeError):
+            mk.maxk_forward(x, k, return_index=True, out=(sdb[:, :8], sib))
     finally:
         dist.destroy_process_group()

@@ -34,6 +34,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--dataset", default="reddit")
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--opts", default="[{}]", help="JSON list of plan option dicts to compare")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS[args.dataset]
@@ -43,7 +45,7 @@ def main():
     h = graphs.features(n, d, seed=97, device=dev)
     g = graphs.features(n, d, seed=98, device=dev)
     sd, si = mk.maxk_forward(h, k, return_index=True)
-    for world in (1, 2, 4, 8):
+    for world, opts in [(int(w), o) for w in args.worlds.split(",") for o in json.loads(args.opts)]:
         part = RowPartition(ptr, world)
         m = part.max_rows
         td = torch.zeros((part.padded_rows, k), device=dev)
@@ -56,17 +58,18 @@ def main():
         for q in (0, world - 1):
             a, b = part.rows(q)
             lp, li, lv = part.local_csr(ptr, idx, val, q)
-            plan = mk.GraphPlan(lp, li, lv, b - a, li.numel(), d, k, num_cols=part.padded_rows)
+            plan = mk.GraphPlan(lp, li, lv, b - a, li.numel(), d, k, num_cols=part.padded_rows,
+                                options=opts)
             gl = g[a:b].contiguous()
             out = torch.empty((b - a, d), device=dev)
             gr = torch.empty((part.padded_rows, k), device=dev)
             tf = timeit(lambda: plan.forward(td, tix, out))
             tb = timeit(lambda: plan.backward(gl, tix, gr))
             worst = max(worst, tf + tb)
-            print(json.dumps({"world": world, "rank": q, "edges": li.numel(), "fwd_ms": tf,
+            print(json.dumps({"world": world, "opts": opts, "rank": q, "edges": li.numel(), "fwd_ms": tf,
                               "bwd_ms": tb, "info": plan.info()}), flush=True)
             del plan
-        print(json.dumps({"world": world, "compute_ms_max": worst,
+        print(json.dumps({"world": world, "opts": opts, "compute_ms_max": worst,
                           "edges_per_s_compute_only": 2 * e / (worst * 1e-3)}), flush=True)
 
 
