@@ -47,7 +47,8 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
 // with wrong numerics. 1: forward ds_add_u64 of the f64 bits; 2: forward without LDS
 // updates; 3: backward ds_add_u32 of the f32 bits instead of the read + CAS; 4: backward
 // ds_add_f32 (correct sums, timing of the native LDS float atomic); 5: backward without LDS
-// updates; 6: backward gathers from grad_out row 0 only (L1 hits); 7: both 5 and 6.
+// updates; 6: backward gathers from grad_out row 0 only (L1 hits); 7: both 5 and 6;
+// 9: forward as two ds_add_u32 per element (a split fixed-point accumulator's LDS cost).
 #ifndef MAXK_PROBE
 #define MAXK_PROBE 0
 #endif
@@ -62,6 +63,12 @@ struct LdsAcc<MAXK_ACC_F64> {
                            __HIP_MEMORY_SCOPE_WORKGROUP);
 #elif MAXK_PROBE == 2
     if (v == 1.2345e-30f) lds_add(p, (double)v);  // practically never: keeps the gathers live
+#elif MAXK_PROBE == 9
+    unsigned* u = reinterpret_cast<unsigned*>(p);
+    const int q = __float2int_rz(v * 32768.f);
+    __hip_atomic_fetch_add(u, (unsigned)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(u + 1, (unsigned)__float2int_rz(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
 #else
     lds_add(p, (double)v);
 #endif
