@@ -31,7 +31,7 @@ constexpr int kBwdTasksPerCu = 2;
 constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k atomics) vs its edges
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
-constexpr double kFwdSlotEdgeRate = 1.5e8;  // edges/s one forward work-group slot sustains
+constexpr double kFwdSlotEdgeRate = 1.6e8;  // edges/s one forward slot sustains at k = 16
 constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (S = 2, 4 measured slower)
 // Records past the end of the backward edge list that a wave may read (and ignore).
 constexpr int kBwdRecPad = (kBwdThreads / kWave) * kWave * 16 + kWave;  // MI355X: 8 XCDs, work-groups dealt round-robin (speed only)

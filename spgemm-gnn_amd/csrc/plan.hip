@@ -480,10 +480,15 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     int B = o.fwd_phases;
     p->fwd_persistent = o.fwd_persistent ? 1 : 0;
     p->fwd_rot_ticks = 0;
-    if (B <= 1 && o.fwd_rotate != 2 && k % 4 == 0 && nt > 0) {
-      B = kFwdRotWindows;
+    if (B <= 1 && o.fwd_rotate != 2 && (k % 4 == 0 || p->fwd_chunk3) && nt > 0) {
+      B = o.fwd_rot_windows > 0 ? std::min(o.fwd_rot_windows, 64) : kFwdRotWindows;
+      // one turn of the clock per tile: the measured per-slot rate scales as ~1/k (Reddit:
+      // 2.4e8, 1.65e8, 0.9e8 edges/s per slot at k = 8, 16, 32; best sweep rates 300, 150-200,
+      // 100 M)
+      const double rate = o.fwd_rot_rate > 0 ? o.fwd_rot_rate * 1e6
+                                             : std::min(5e8, std::max(2e7, kFwdSlotEdgeRate * 16.0 / k));
       const double tile_edges = (double)E / nt;
-      const double tile_ticks = tile_edges / kFwdSlotEdgeRate * 1e8;  // s_memrealtime: 100 MHz
+      const double tile_ticks = tile_edges / rate * 1e8;  // s_memrealtime: 100 MHz
       p->fwd_rot_ticks = (int)std::max(1.0, tile_ticks / B);
     }
     if (B == 0) B = 1;

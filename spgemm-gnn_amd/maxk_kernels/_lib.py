@@ -75,7 +75,8 @@ class PlanOptions(ctypes.Structure):
         ("bwd_cas64", _i32),
         ("quad_loads", _i32),
         ("fwd_two_tables", _i32),
-        ("reserved2", _i32 * 2),
+        ("fwd_rot_windows", _i32),
+        ("fwd_rot_rate", _i32),
     ]
 
 

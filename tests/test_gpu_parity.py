@@ -322,6 +322,7 @@ PLAN_OPTIONS = [
     dict(quad_loads=2), dict(quad_loads=1), dict(quad_loads=1, fwd_prefetch=1),
     dict(quad_loads=1, fwd_chunk3=1), dict(bwd_prefetch=1, bwd_waves=16),
     dict(fwd_two_tables=1), dict(fwd_two_tables=2), dict(fwd_two_tables=1, fwd_prefetch=1),
+    dict(fwd_rot_windows=64), dict(fwd_rot_windows=3, fwd_rot_rate=1),
 ]
 
 
