@@ -507,7 +507,18 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     p->device_bytes += sizeof(int32_t) * zrows.size();
   }
 
-  if (p->fwd_chunk3 && NC > 0) {
+  MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
+                 "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
+  // Two tables (no record pack): Reddit k = 32 2.65 -> 2.53 ms, k = 64 4.98 -> 4.92 (k = 16:
+  // 1.35 vs 1.39 packed); and where the per-call pack of all NC records costs more than it
+  // saves, below ~128 edges per column (an 8-GPU row shard of Reddit at k = 16: 0.221 ->
+  // 0.207 ms)
+  p->fwd_two_tables = !p->fwd_chunk3 && k % 4 == 0 &&
+                      (o.fwd_two_tables == 1 ||
+                       (o.fwd_two_tables == 0 && (k >= 32 || E < 128ll * std::max(NC, 1))));
+  if (p->fwd_two_tables) {
+    // no workspace: the kernel gathers from sp_data / sp_index
+  } else if (p->fwd_chunk3 && NC > 0) {
     const int b = (k + 2) / 3 * 16;
     if (o.fwd_record_bytes != 0 && o.fwd_record_bytes < b) {
       set_error("maxk_plan_create: fwd_record_bytes too small for the lane-chunk records");
@@ -562,10 +573,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // 8-B edge words gain nothing: forward only on request)
   p->bwd_quad = o.quad_loads != 2;
   p->fwd_quad = o.quad_loads == 1;
-  MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
-                 "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
-  // (Reddit k = 32: 2.65 -> 2.53 ms, k = 64: 4.98 -> 4.92; k = 16: 1.35 vs 1.39 packed)
-  p->fwd_two_tables = o.fwd_two_tables == 1 || (o.fwd_two_tables == 0 && k >= 32);
   if (p->bwd_cas64) p->bwd_ks = nslots + (o.bwd_acc_pad == 1 ? 4 : 0);
   else p->bwd_ks = nslots + ((packed && o.bwd_acc_pad == 2) ? 0 : 1);
   p->bwd_sel_lds = packed && o.bwd_sel_lds != 2 ? 1 : 0;

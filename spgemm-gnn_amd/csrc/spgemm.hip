@@ -999,7 +999,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
   const size_t lds = fwd_lds_bytes(R, D, plan->fwd_acc);
   const int rec_bytes = plan->fwd_rec_bytes;
   // two tables: values read straight from sp_data (4k-byte rows), selectors from sp_index
-  const bool two = plan->fwd_two_tables && !plan->fwd_chunk3 && k % 4 == 0;
+  const bool two = plan->fwd_two_tables;  // the plan only sets it with k % 4 == 0, no chunks
   const uint8_t* seltab = two ? sp_index : nullptr;
   const uint8_t* recp = two ? reinterpret_cast<const uint8_t*>(sp_data) : plan->fwd_rec;
   const int rec_bytes_eff = two ? 4 * k : rec_bytes;
