@@ -123,3 +123,26 @@ def test_baseline_library_exports_its_header():
     ms = ctypes.c_float()
     assert bl.maxk_spmm_rocsparse(None, None, None, None, None, -1, 0, 8, 0, 0,
                                   ctypes.byref(ms), None) == -1
+
+
+def _struct_fields(name):
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct " + name + r"\s*\{(.*?)\}\s*" + name + ";", text, re.S)
+    fields = []
+    for decl in body.group(1).split(";"):
+        m = re.search(r"\b(int32_t|int64_t)\s+(\w+)(\[(\d+)\])?\s*$", decl.strip())
+        if m:
+            fields.append((m.group(2), m.group(1), int(m.group(4) or 1)))
+    return fields
+
+
+@pytest.mark.parametrize("cname,pycls", [("maxk_plan_options", "PlanOptions"),
+                                          ("maxk_plan_info", "PlanInfo")])
+def test_ctypes_structs_mirror_header(cname, pycls):
+    """The ctypes mirrors must match the C structs field by field (names, widths, order)."""
+    fields = _struct_fields(cname)
+    py = getattr(_lib, pycls)._fields_
+    assert [f[0] for f in fields] == [f[0] for f in py]
+    for (name, ctype, count), (_, pytype) in zip(fields, py):
+        width = 4 if ctype == "int32_t" else 8
+        assert ctypes.sizeof(pytype) == width * count, name
