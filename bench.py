@@ -152,6 +152,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--dataset", default="reddit", choices=sorted(graphs.DATASETS))
     ap.add_argument("--k", type=int, default=16)
+    ap.add_argument("--phases", type=int, default=1,
+                    help="column phases of the N > 1 exchange (all-gather / reduce-scatter of "
+                         "one phase overlapping the other's compute; 1 = one-shot, the default: "
+                         "2 phases cost +14 %% per-rank compute at W=8, tools/shard_time.py)")
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--cpu-sample", type=float, default=1.0,
                     help="fraction of E timed per direction for the CPU baseline")
@@ -182,7 +186,7 @@ def main():
     torch.cuda.synchronize()
     log(f"graph {args.dataset}: N={n} E={e} generated in {time.perf_counter() - t0:.1f}s")
 
-    part = RowPartition(ptr, world)
+    part = RowPartition(ptr, world, phases=args.phases if world > 1 else 1)
     r0, r1 = part.rows(rank)
     h = graphs.features(n, d, seed=97, device=dev)[r0:r1].contiguous()
     g = graphs.features(n, d, seed=98, device=dev)[r0:r1].contiguous()
@@ -208,17 +212,22 @@ def main():
         shard = ShardedAggregation(part, rank, ptr, idx, val, d, k)
         # the top-k lands in the shard's padded send buffers: the exchange copies nothing
         sp_data, sp_index = mk.maxk_forward(h, k, return_index=True, out=shard.local_buffers())
-        plan = shard.plan
-        info = plan.info()
+        plans = shard.plans
+        info = plans[0].info()
+        info["num_edges"] = sum(pl.info()["num_edges"] for pl in plans)
         out = torch.empty((r1 - r0, d), dtype=torch.float32, device=dev)
         grad_sp = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
         shard.gather(sp_data, sp_index)
+        nc = part.phase_cols
 
-        def fwd():
-            plan.forward(shard.table_data, shard.table_index, out)
+        def fwd():  # this rank's kernels alone (all phases), no collectives
+            for q, pl in enumerate(plans):
+                pl.forward(shard.table_data[q * nc:(q + 1) * nc],
+                           shard.table_index[q * nc:(q + 1) * nc], out, accumulate=q > 0)
 
         def bwd():
-            plan.backward(g, shard.table_index, grad_sp)
+            for q, pl in enumerate(plans):
+                pl.backward(g, shard.table_index[q * nc:(q + 1) * nc], grad_sp[q * nc:(q + 1) * nc])
 
         def step():
             shard.forward(sp_data, sp_index)

@@ -250,7 +250,7 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     int phases, int phase, const uint2* __restrict__ cv,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
     const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
-    int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab) {
+    int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab, int accum) {
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
@@ -278,12 +278,12 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   t.e0 = phase_off[ti * (phases + 1) + phase];
   t.e1 = phase_off[ti * (phases + 1) + phase + 1];
   }
-  if (phase > 0 && t.e0 == t.e1) continue;  // nothing to add in this phase (uniform)
+  if ((phase > 0 || accum) && t.e0 == t.e1) continue;  // nothing to add (uniform)
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
   const int n = nrows * D;
   __syncthreads();  // the previous task's write-back has finished reading acc
-  if (phase > 0 && !split) {
+  if ((phase > 0 || accum) && !split) {  // continue from the stored rows
     const float* src = out + (size_t)t.row0 * D;
     for (int i = threadIdx.x; i < n; i += NT) acc[i] = T(src[i]);
   } else {
@@ -975,10 +975,10 @@ static int check_plan(const maxk_plan* plan, const int32_t* ptr, const int32_t* 
   return MAXK_OK;
 }
 
-extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
-                                   const int32_t* idx, const float* val,
-                                   const float* sp_data, const uint8_t* sp_index, float* out,
-                                   int32_t N, int64_t E, int32_t k, int32_t D, void* stream) {
+static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const int32_t* idx,
+                               const float* val, const float* sp_data, const uint8_t* sp_index,
+                               float* out, int32_t N, int64_t E, int32_t k, int32_t D,
+                               void* stream, int accum) {
   MAXK_CHECK_ARG(N >= 0 && E >= 0, "maxk_spgemm_forward: negative size");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_spgemm_forward: dim_origin must be in [1, 256]");
   MAXK_CHECK_ARG(k >= 1 && k <= D, "k must be between 1 and input dimension");
@@ -989,7 +989,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
                  "maxk_spgemm_forward: null pointer");
   (void)val;  // the plan holds the permuted snapshot of (idx, val)
   hipStream_t s = (hipStream_t)stream;
-  if (plan->n_zero_rows > 0) {
+  if (plan->n_zero_rows > 0 && !accum) {  // split rows are summed atomically into zeroed rows
     hipLaunchKernelGGL(zero_rows_kernel, dim3(plan->n_zero_rows), dim3(256), 0, s,
                        plan->zero_rows, plan->n_zero_rows, out, D);
     MAXK_LAUNCH_CHECK("zero_rows launch");
@@ -1033,7 +1033,7 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
       hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU, NT, FL>), dim3(g), dim3(NT), lds, s, \
                          plan->fwd_tasks, plan->n_fwd_tasks, plan->fwd_phase_off, B, b,   \
                          plan->fwd_cv, sp_data, sp_index, recp,                           \
-                         rec_bytes_eff, out, D, k, R, rot, seltab);                       \
+                         rec_bytes_eff, out, D, k, R, rot, seltab, accum);                \
   } while (0)
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \
@@ -1091,6 +1091,21 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
 #undef FWD_LAUNCH1
   MAXK_LAUNCH_CHECK("spgemm_fwd launch");
   return MAXK_OK;
+}
+
+extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
+                                   const int32_t* idx, const float* val,
+                                   const float* sp_data, const uint8_t* sp_index, float* out,
+                                   int32_t N, int64_t E, int32_t k, int32_t D, void* stream) {
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream, 0);
+}
+
+extern "C" int maxk_spgemm_forward_acc(const maxk_plan* plan, const int32_t* ptr,
+                                       const int32_t* idx, const float* val,
+                                       const float* sp_data, const uint8_t* sp_index,
+                                       float* out, int32_t N, int64_t E, int32_t k, int32_t D,
+                                       void* stream) {
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream, 1);
 }
 
 extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,

@@ -36,6 +36,8 @@ SIGNATURES = {
     "maxk_plan_destroy": (ctypes.c_int, [_vp]),
     "maxk_spgemm_forward": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
                                            _i32, _i32, _vp]),
+    "maxk_spgemm_forward_acc": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
+                                               _i32, _i32, _vp]),
     "maxk_sspmm_backward": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
                                            _i32, _i32, _vp]),
     "maxk_dense_spmm_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),

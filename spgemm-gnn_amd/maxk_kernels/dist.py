@@ -7,30 +7,37 @@ exchange per direction:
 * partition: contiguous row ranges balanced by nnz; rank q owns rows [start_q, end_q),
   their CSR slice (columns keep pointing at any node) and computes the top-k of its own
   rows (weights are replicated);
-* forward : RCCL all-gathers of the k-sparse CBSR block (sp_data f32 and sp_index u8,
-  coalesced into one group call) straight into the tables the kernels read, padded to
-  W x max_rows rows; the rank's top-k can be written directly into its send buffers
-  (``local_buffers``), so the exchange moves no extra copies. Then the local SpGEMM over
-  the rank's rows with a rectangular plan whose column ids are remapped into that padded
-  table (remapping is done once, at partition time);
+* forward : RCCL all-gathers of the k-sparse CBSR block (sp_data f32 and sp_index u8)
+  straight into the tables the kernels read; the rank's top-k can be written directly into
+  its send buffers (``local_buffers``), so the exchange moves no extra copies. Then the
+  local SpGEMM over the rank's rows with rectangular plans whose column ids are remapped
+  into the gathered table (once, at partition time);
 * backward: the local SSpMM produces a partial grad_sp for every (padded) column; an
   RCCL reduce-scatter (sum) returns each rank its own rows' gradient.
+
+Column phases (``phases`` P > 1): every rank's rows are cut into P parts and the table is
+laid out phase-major (phase p holds part p of every rank), so each phase is one all-gather
+and one reduce-scatter of its own. The rank keeps one plan per phase (its edges split by the
+phase of their column). The all-gather of phase p+1 then runs while the SpGEMM of phase p
+(accumulating into the same output) computes, and the reduce-scatter of phase p while the
+SSpMM of phase p+1 computes. P = 1 is the plain one-shot exchange.
 
 Bytes exchanged per step are 5kN (all-gathers) + 4kN (reduce-scatter), i.e. 18.6 MB +
 14.9 MB for Reddit at k=16, against 238 MB for all-gathering dense features.
 """
 from __future__ import annotations
 
-from typing import Callable, Optional
+from typing import Callable, List, Optional
 
 import torch
 import torch.distributed as dist
 
 
 class RowPartition:
-    """Contiguous destination-row ranges with ~equal nnz per rank."""
+    """Contiguous destination-row ranges with ~equal nnz per rank, and the phase-major
+    layout of the all-gathered CBSR table (``phases`` parts per rank)."""
 
-    def __init__(self, ptr: torch.Tensor, world_size: int):
+    def __init__(self, ptr: torch.Tensor, world_size: int, phases: int = 1):
         p = ptr.detach().to("cpu", torch.int64)
         n = p.numel() - 1
         e = int(p[-1])
@@ -45,17 +52,31 @@ class RowPartition:
         self.bounds = b                      # [W+1] row boundaries
         counts = b[1:] - b[:-1]
         self.max_rows = max(1, int(counts.max()))
-        self.padded_rows = w * self.max_rows
+        self.phases = max(1, int(phases))
+        self.phase_rows = -(-self.max_rows // self.phases)   # rows of a rank in one phase
+        self.phase_cols = w * self.phase_rows                 # table rows of one phase
+        self.send_rows = self.phases * self.phase_rows        # >= max_rows
+        self.padded_rows = self.phases * self.phase_cols
 
     def rows(self, rank: int):
         return int(self.bounds[rank]), int(self.bounds[rank + 1])
 
+    def _position(self, q: torch.Tensor, off: torch.Tensor) -> torch.Tensor:
+        ph = off // self.phase_rows
+        return ph * self.phase_cols + q * self.phase_rows + (off - ph * self.phase_rows)
+
     def remap_columns(self, idx: torch.Tensor) -> torch.Tensor:
-        """Global column id -> position in the padded all-gather table."""
+        """Global column id -> position in the padded (phase-major) all-gather table."""
         b = self.bounds.to(idx.device)
         c = idx.to(torch.int64)
         q = torch.searchsorted(b, c, right=True) - 1
-        return (q * self.max_rows + (c - b[q])).to(torch.int32)
+        return self._position(q, c - b[q]).to(torch.int32)
+
+    def table_positions(self, rank: int, device=None) -> torch.Tensor:
+        """Table rows holding rank's nodes, in node order (int64 [n_rank])."""
+        a, b = self.rows(rank)
+        off = torch.arange(b - a, dtype=torch.int64, device=device)
+        return self._position(torch.full_like(off, rank), off)
 
     def local_csr(self, ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, rank: int):
         """(ptr, remapped idx, val) of rank's rows; ptr rebased to 0."""
@@ -66,17 +87,34 @@ class RowPartition:
         lval = val[e0:e1].contiguous()
         return lptr, lidx, lval
 
+    def phase_csr(self, lptr: torch.Tensor, lidx: torch.Tensor, lval: torch.Tensor, phase: int):
+        """The edges of a local CSR (remapped columns) whose column lies in ``phase``, with
+        columns rebased to that phase's table block [0, phase_cols)."""
+        lo = phase * self.phase_cols
+        keep = (lidx >= lo) & (lidx < lo + self.phase_cols)
+        n = lptr.numel() - 1
+        rows = torch.repeat_interleave(torch.arange(n, device=lptr.device),
+                                       (lptr[1:] - lptr[:-1]).to(torch.int64))
+        cnt = torch.bincount(rows[keep], minlength=n)
+        pptr = torch.zeros(n + 1, dtype=torch.int64, device=lptr.device)
+        pptr[1:] = torch.cumsum(cnt, 0)
+        return (pptr.to(torch.int32).contiguous(), (lidx[keep] - lo).to(torch.int32).contiguous(),
+                lval[keep].contiguous())
 
-FwdFn = Callable[[torch.Tensor, torch.Tensor], torch.Tensor]
-BwdFn = Callable[[torch.Tensor, torch.Tensor], torch.Tensor]
+
+# injected per-phase compute (CPU tests): fwd(phase, table_data_p, table_index_p, out) -> out
+# (out is None for phase 0, else the output to accumulate into); bwd(phase, grad_out,
+# table_index_p) -> grad for the phase's table block
+FwdFn = Callable[[int, torch.Tensor, torch.Tensor, Optional[torch.Tensor]], torch.Tensor]
+BwdFn = Callable[[int, torch.Tensor, torch.Tensor], torch.Tensor]
 
 
 class ShardedAggregation:
     """One rank's share of Y = A densify(sp) and of its SSpMM backward.
 
-    ``fwd(table_data, table_index) -> out_local`` and ``bwd(grad_out_local, table_index)
-    -> grad_table`` default to the gfx950 kernels through a rectangular GraphPlan; tests
-    on CPU (gloo) inject checker callables to exercise the partition and the collectives.
+    ``fwd``/``bwd`` default to the gfx950 kernels through one rectangular GraphPlan per
+    column phase; tests on CPU (gloo) inject checker callables to exercise the partition,
+    the phase layout and the collectives.
     """
 
     def __init__(self, part: RowPartition, rank: int, ptr: torch.Tensor, idx: torch.Tensor,
@@ -89,56 +127,92 @@ class ShardedAggregation:
         self.n_local = self.r1 - self.r0
         self.ptr, self.idx, self.val = part.local_csr(ptr, idx, val, rank)
         dev = self.ptr.device
-        m, k = part.max_rows, self.dim_k
+        P, k = part.phases, self.dim_k
         # padded send buffers (rows >= n_local stay zero) and the all-gathered tables
-        self.send_data = torch.zeros((m, k), dtype=torch.float32, device=dev)
-        self.send_index = torch.zeros((m, k), dtype=torch.uint8, device=dev)
+        self.send_data = torch.zeros((part.send_rows, k), dtype=torch.float32, device=dev)
+        self.send_index = torch.zeros((part.send_rows, k), dtype=torch.uint8, device=dev)
         self.table_data = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
         self.table_index = torch.empty((part.padded_rows, k), dtype=torch.uint8, device=dev)
-        self.grad_local = torch.empty((m, k), dtype=torch.float32, device=dev)
-        self.plan = None
+        self.grad_table = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
+        self.grad_local = torch.empty((part.send_rows, k), dtype=torch.float32, device=dev)
+        self.plans: List = []
         if fwd is None or bwd is None:
             from .ops import GraphPlan
-            self.plan = GraphPlan(self.ptr, self.idx, self.val, self.n_local, self.idx.numel(),
-                                  self.dim_origin, self.dim_k, num_cols=part.padded_rows)
-        self._fwd = fwd or (lambda d, i: self.plan.forward(d, i))
-        self._bwd = bwd or (lambda g, i: self.plan.backward(g, i))
+            for p in range(P):
+                pp, pi, pv = part.phase_csr(self.ptr, self.idx, self.val, p)
+                self.plans.append(GraphPlan(pp, pi, pv, self.n_local, pi.numel(),
+                                            self.dim_origin, self.dim_k,
+                                            num_cols=part.phase_cols))
+        self._fwd = fwd or (lambda p, d, i, out: self.plans[p].forward(
+            d, i, out, accumulate=out is not None))
+        self._bwd = bwd or (lambda p, g, i: self.plans[p].backward(
+            g, i, self._slice(self.grad_table, p)))
+
+    @property
+    def plan(self):
+        """The plan of a one-phase partition (bench.py's per-kernel timing)."""
+        return self.plans[0] if len(self.plans) == 1 else None
+
+    def _slice(self, table: torch.Tensor, p: int) -> torch.Tensor:
+        c = self.part.phase_cols
+        return table[p * c: (p + 1) * c]
+
+    def _send_slice(self, buf: torch.Tensor, p: int) -> torch.Tensor:
+        r = self.part.phase_rows
+        return buf[p * r: (p + 1) * r]
 
     def local_buffers(self):
         """(sp_data, sp_index) views [n_local, k] of the send buffers: write this rank's
         top-k here (``maxk_forward(h, k, out=...)``) and ``gather`` sends them as they are."""
         return self.send_data[: self.n_local], self.send_index[: self.n_local]
 
-    def gather(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> None:
-        """All-gather this rank's CBSR rows into the padded tables (RCCL over xGMI)."""
+    def _stage(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> None:
         n = self.n_local
         if sp_data_local.data_ptr() != self.send_data.data_ptr():
             self.send_data[:n].copy_(sp_data_local)
         if sp_index_local.data_ptr() != self.send_index.data_ptr():
             self.send_index[:n].copy_(sp_index_local)
-        cm = getattr(dist, "_coalescing_manager", None)
-        if cm is not None and self.table_data.is_cuda:
-            with cm(group=self.group, device=self.table_data.device):
-                dist.all_gather_into_tensor(self.table_data, self.send_data, group=self.group)
-                dist.all_gather_into_tensor(self.table_index, self.send_index, group=self.group)
-        else:
-            dist.all_gather_into_tensor(self.table_data, self.send_data, group=self.group)
-            dist.all_gather_into_tensor(self.table_index, self.send_index, group=self.group)
+
+    def _gather_phase(self, p: int, async_op: bool):
+        w1 = dist.all_gather_into_tensor(self._slice(self.table_data, p),
+                                         self._send_slice(self.send_data, p),
+                                         group=self.group, async_op=async_op)
+        w2 = dist.all_gather_into_tensor(self._slice(self.table_index, p),
+                                         self._send_slice(self.send_index, p),
+                                         group=self.group, async_op=async_op)
+        return (w1, w2)
+
+    def gather(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> None:
+        """All-gather this rank's CBSR rows into the padded tables (RCCL over xGMI)."""
+        self._stage(sp_data_local, sp_index_local)
+        for p in range(self.part.phases):
+            self._gather_phase(p, async_op=False)
 
     def forward(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> torch.Tensor:
-        self.gather(sp_data_local, sp_index_local)
-        return self._fwd(self.table_data, self.table_index)
+        self._stage(sp_data_local, sp_index_local)
+        P = self.part.phases
+        works = [self._gather_phase(p, async_op=True) for p in range(P)]
+        out = None
+        for p in range(P):
+            for wk in works[p]:
+                wk.wait()   # the compute stream waits for phase p only
+            out = self._fwd(p, self._slice(self.table_data, p), self._slice(self.table_index, p),
+                            out)
+        return out
 
     def backward(self, grad_out_local: torch.Tensor) -> torch.Tensor:
-        grad_table = self._bwd(grad_out_local.contiguous(), self.table_index)
-        dist.reduce_scatter_tensor(self.grad_local, grad_table, op=dist.ReduceOp.SUM,
-                                   group=self.group)
+        g = grad_out_local.contiguous()
+        works = []
+        for p in range(self.part.phases):
+            gp = self._bwd(p, g, self._slice(self.table_index, p))
+            works.append(dist.reduce_scatter_tensor(self._send_slice(self.grad_local, p), gp,
+                                                    op=dist.ReduceOp.SUM, group=self.group,
+                                                    async_op=True))
+        for wk in works:
+            wk.wait()
         return self.grad_local[: self.n_local]
 
     def unpad_table(self, table: torch.Tensor) -> torch.Tensor:
-        """Padded [W*max_rows, ...] table -> natural node order [N, ...] (tests/inspection)."""
-        parts = []
-        for q in range(self.part.world_size):
-            a, b = self.part.rows(q)
-            parts.append(table[q * self.part.max_rows: q * self.part.max_rows + (b - a)])
-        return torch.cat(parts)
+        """Padded phase-major table -> natural node order [N, ...] (tests/inspection)."""
+        return torch.cat([table[self.part.table_positions(q, table.device)]
+                          for q in range(self.part.world_size)])

@@ -148,15 +148,19 @@ class GraphPlan:
                                           self.dim_k, ctypes.byref(opts), _stream(),
                                           ctypes.byref(self.handle)), "maxk_plan_create")
 
-    def forward(self, sp_data, sp_index, out=None) -> torch.Tensor:
-        """SpGEMM with this plan: sp tables [num_cols, k] -> out [num_rows, D]."""
+    def forward(self, sp_data, sp_index, out=None, accumulate: bool = False) -> torch.Tensor:
+        """SpGEMM with this plan: sp tables [num_cols, k] -> out [num_rows, D];
+        ``accumulate=True`` adds into the given ``out`` instead of overwriting it."""
         ptr, idx, val = self._refs
         if out is None:
+            if accumulate:
+                raise RuntimeError("accumulate=True needs an out tensor")
             out = torch.empty((self.num_rows, self.dim_origin), dtype=torch.float32,
                               device=sp_data.device)
-        check(lib.maxk_spgemm_forward(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
-                                      _p(sp_index), _p(out), self.num_rows, self.num_edges,
-                                      self.dim_k, self.dim_origin, _stream()), "spgemm_forward")
+        fn = lib.maxk_spgemm_forward_acc if accumulate else lib.maxk_spgemm_forward
+        check(fn(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data), _p(sp_index), _p(out),
+                 self.num_rows, self.num_edges, self.dim_k, self.dim_origin, _stream()),
+              "spgemm_forward")
         return out
 
     def backward(self, grad_out, sp_index, grad_sp=None) -> torch.Tensor:

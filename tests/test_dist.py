@@ -23,10 +23,26 @@ def test_partition_balances_nnz_and_remaps():
         nnz = [int(ptr[part.rows(q)[1]] - ptr[part.rows(q)[0]]) for q in range(w)]
         assert sum(nnz) == 80_000
         assert max(nnz) - min(nnz) <= 2 * int((ptr[1:] - ptr[:-1]).max())
-        pos = part.remap_columns(torch.arange(3000, dtype=torch.int32))
-        # the remap is injective into [0, padded_rows) and order-preserving per owner
-        assert torch.unique(pos).numel() == 3000 and int(pos.max()) < part.padded_rows
-        assert bool((pos[1:] > pos[:-1]).all())
+        for phases in (1, 2, 3):
+            part = RowPartition(ptr, w, phases=phases)
+            pos = part.remap_columns(torch.arange(3000, dtype=torch.int32))
+            # the remap is injective into [0, padded_rows) and, per owner, order-preserving
+            assert torch.unique(pos).numel() == 3000 and int(pos.max()) < part.padded_rows
+            for q in range(w):
+                a, b = part.rows(q)
+                assert bool((pos[a + 1:b] > pos[a:b - 1]).all())
+                assert torch.equal(part.table_positions(q), pos[a:b].long())
+            if phases == 1:
+                assert bool((pos[1:] > pos[:-1]).all())
+            # a phase's CSR keeps exactly the edges whose column lies in that phase
+            lp, li, lv = part.local_csr(ptr, idx, graphs.sage_mean_values(ptr), 0)
+            tot = 0
+            for ph in range(phases):
+                pp, pi, pv = part.phase_csr(lp, li, lv, ph)
+                assert int(pp[-1]) == pi.numel() == pv.numel()
+                assert pi.numel() == 0 or (int(pi.min()) >= 0 and int(pi.max()) < part.phase_cols)
+                tot += pi.numel()
+            assert tot == li.numel()
 
 
 def _free_port():
@@ -37,7 +53,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, ret):
+def _worker(rank, world, port, ret, phases=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -47,27 +63,34 @@ def _worker(rank, world, port, ret):
         val = graphs.sage_mean_values(ptr)
         x = graphs.features(n, d, seed=1)
         g = graphs.features(n, d, seed=2)
-        part = RowPartition(ptr, world)
+        part = RowPartition(ptr, world, phases=phases)
         r0, r1 = part.rows(rank)
         sd, si = oracle.maxk(x[r0:r1].numpy(), k)
+        nc = part.phase_cols
 
-        def fwd(td, ti):
-            lptr, lidx, lval = shard.ptr, shard.idx, shard.val
-            # oracle reads CBSR rows by column id; pad local rows to padded_rows
-            full_ptr = np.full(part.padded_rows + 1, lptr[-1].item(), np.int32)
+        def phase_graph(ph):
+            lptr, lidx, lval = part.phase_csr(shard.ptr, shard.idx, shard.val, ph)
+            # the oracle indexes CBSR rows by column id: pad the local rows to the block size
+            nr = max(nc, r1 - r0)
+            full_ptr = np.full(nr + 1, lptr[-1].item(), np.int32)
             full_ptr[: lptr.numel()] = lptr.numpy()
-            y = oracle.spgemm_forward(full_ptr, lidx.numpy(), lval.numpy(), td.numpy(),
-                                      ti.numpy(), d)
-            return torch.from_numpy(y[: r1 - r0].copy())
+            return full_ptr, lidx.numpy(), lval.numpy(), nr
 
-        def bwd(gl, ti):
-            lptr, lidx, lval = shard.ptr, shard.idx, shard.val
-            full_ptr = np.full(part.padded_rows + 1, lptr[-1].item(), np.int32)
-            full_ptr[: lptr.numel()] = lptr.numpy()
-            gfull = np.zeros((part.padded_rows, d), np.float32)
+        def fwd(ph, td, ti, out):
+            fp, li, lv, nr = phase_graph(ph)
+            tdp = np.zeros((nr, k), np.float32)
+            tip = np.zeros((nr, k), np.uint8)
+            tdp[:nc], tip[:nc] = td.numpy(), ti.numpy()
+            y = torch.from_numpy(oracle.spgemm_forward(fp, li, lv, tdp, tip, d)[: r1 - r0].copy())
+            return y if out is None else out + y
+
+        def bwd(ph, gl, ti):
+            fp, li, lv, nr = phase_graph(ph)
+            gfull = np.zeros((nr, d), np.float32)
             gfull[: r1 - r0] = gl.numpy()
-            return torch.from_numpy(oracle.sspmm_backward(full_ptr, lidx.numpy(), lval.numpy(),
-                                                          gfull, ti.numpy()))
+            tip = np.zeros((nr, k), np.uint8)
+            tip[:nc] = ti.numpy()
+            return torch.from_numpy(oracle.sspmm_backward(fp, li, lv, gfull, tip)[:nc].copy())
 
         shard = ShardedAggregation(part, rank, ptr, idx, val, d, k, fwd=fwd, bwd=bwd)
         y = shard.forward(torch.from_numpy(sd), torch.from_numpy(si))
@@ -78,12 +101,12 @@ def _worker(rank, world, port, ret):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_aggregation_matches_single(world):
+@pytest.mark.parametrize("world,phases", [(2, 1), (2, 2), (3, 2)])
+def test_sharded_aggregation_matches_single(world, phases):
     from oracle import oracle
     mgr = mp.Manager()
     ret = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), ret), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), ret, phases), nprocs=world, join=True)
     n, d, k = 700, 32, 8
     ptr, idx = graphs.synthetic_csr(n, 15_000, seed=3)
     val = graphs.sage_mean_values(ptr)

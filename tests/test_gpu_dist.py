@@ -26,9 +26,11 @@ def _graph(n=6000, e=150_000, seed=41):
     return p, i, graphs.sage_mean_values(p)
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("world,phases", [(2, 1), (3, 1), (8, 1), (2, 2), (8, 2), (3, 3)])
 @pytest.mark.parametrize("k", [16, 32])
-def test_emulated_partition_matches_oracle(gpu, world, k):
+def test_emulated_partition_matches_oracle(gpu, world, phases, k):
+    """Every rank's per-phase rectangular plans (columns remapped into the phase-major
+    padded table) on one GPU; the all-gather / reduce-scatter done with tensor ops."""
     p, i, v = _graph()
     n, d = p.numel() - 1, 256
     x = graphs.features(n, d, seed=5)
@@ -38,30 +40,55 @@ def test_emulated_partition_matches_oracle(gpu, world, k):
     ref_b, mag_b = oracle.sspmm_backward(p.numpy(), i.numpy(), v.numpy(), g.numpy(), oi,
                                          with_mag=True)
     ptr, idx, val = p.to(gpu), i.to(gpu), v.to(gpu)
-    part = RowPartition(ptr, world)
-    m = part.max_rows
+    part = RowPartition(ptr, world, phases=phases)
     # the padded all-gather table every rank would hold
     table_d = torch.zeros((part.padded_rows, k), device=gpu)
     table_i = torch.zeros((part.padded_rows, k), dtype=torch.uint8, device=gpu)
     for q in range(world):
         a, b = part.rows(q)
-        table_d[q * m: q * m + (b - a)] = torch.from_numpy(od[a:b]).to(gpu)
-        table_i[q * m: q * m + (b - a)] = torch.from_numpy(oi[a:b]).to(gpu)
+        pos = part.table_positions(q, gpu)
+        table_d[pos] = torch.from_numpy(od[a:b]).to(gpu)
+        table_i[pos] = torch.from_numpy(oi[a:b]).to(gpu)
     y = torch.empty((n, d), device=gpu)
     grad_table = torch.zeros((part.padded_rows, k), device=gpu)
+    nc = part.phase_cols
     for q in range(world):
         a, b = part.rows(q)
         lp, li, lv = part.local_csr(ptr, idx, val, q)
-        plan = mk.GraphPlan(lp, li, lv, b - a, li.numel(), d, k, num_cols=part.padded_rows)
-        y[a:b] = plan.forward(table_d, table_i)
-        grad_table += plan.backward(g[a:b].contiguous().to(gpu), table_i)   # reduce-scatter
-    gs = torch.cat([grad_table[q * m: q * m + (part.rows(q)[1] - part.rows(q)[0])]
-                    for q in range(world)])
+        out = torch.empty((b - a, d), device=gpu)
+        for ph in range(phases):
+            pp, pi, pv = part.phase_csr(lp, li, lv, ph)
+            plan = mk.GraphPlan(pp, pi, pv, b - a, pi.numel(), d, k, num_cols=nc)
+            plan.forward(table_d[ph * nc:(ph + 1) * nc], table_i[ph * nc:(ph + 1) * nc], out,
+                         accumulate=ph > 0)
+            grad_table[ph * nc:(ph + 1) * nc] += plan.backward(                # reduce-scatter
+                g[a:b].contiguous().to(gpu), table_i[ph * nc:(ph + 1) * nc])
+        y[a:b] = out
+    gs = torch.cat([grad_table[part.table_positions(q, gpu)] for q in range(world)])
     ok, worst = oracle.close_enough(y.cpu().numpy(), ref_f, mag_f)
     assert ok, worst
     # per-rank partials summed in f32: bound by the summed magnitude
     ok, worst = oracle.close_enough(gs.cpu().numpy(), ref_b, mag_b, rtol=2e-5)
     assert ok, worst
+
+
+def test_forward_accumulate_vs_oracle(gpu):
+    """maxk_spgemm_forward_acc: out += A densify(sp) on top of prior values."""
+    p, i, v = _graph(n=3000, e=60_000, seed=43)
+    n, d, k = p.numel() - 1, 256, 16
+    x = graphs.features(n, d, seed=9)
+    od, oi = oracle.maxk(x.numpy(), k)
+    ref, mag = oracle.spgemm_forward(p.numpy(), i.numpy(), v.numpy(), od, oi, d, with_mag=True)
+    prior = graphs.features(n, d, seed=10)
+    ptr, idx, val = p.to(gpu), i.to(gpu), v.to(gpu)
+    plan = mk.GraphPlan(ptr, idx, val, n, i.numel(), d, k)
+    out = prior.clone().to(gpu)
+    plan.forward(torch.from_numpy(od).to(gpu), torch.from_numpy(oi).to(gpu), out, accumulate=True)
+    ok, worst = oracle.close_enough(out.cpu().numpy(), ref + prior.numpy(),
+                                    mag + np.abs(prior.numpy()))
+    assert ok, worst
+    with pytest.raises(RuntimeError):
+        plan.forward(torch.from_numpy(od).to(gpu), torch.from_numpy(oi).to(gpu), accumulate=True)
 
 
 def _free_port():
@@ -72,7 +99,8 @@ def _free_port():
     return port
 
 
-def test_sharded_aggregation_rccl_world1(gpu):
+@pytest.mark.parametrize("phases", [1, 2])
+def test_sharded_aggregation_rccl_world1(gpu, phases):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
@@ -83,7 +111,7 @@ def test_sharded_aggregation_rccl_world1(gpu):
         x = graphs.features(n, d, seed=7).to(gpu)
         g = graphs.features(n, d, seed=8).to(gpu)
         sd, si = mk.maxk_forward(x, k, return_index=True)
-        part = RowPartition(ptr, 1)
+        part = RowPartition(ptr, 1, phases=phases)
         shard = ShardedAggregation(part, 0, ptr, idx, val, d, k)
         y = shard.forward(sd, si)
         gs = shard.backward(g)
