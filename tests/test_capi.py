@@ -146,3 +146,24 @@ def test_ctypes_structs_mirror_header(cname, pycls):
     for (name, ctype, count), (_, pytype) in zip(fields, py):
         width = 4 if ctype == "int32_t" else 8
         assert ctypes.sizeof(pytype) == width * count, name
+
+
+def test_header_is_plain_c(tmp_path):
+    """include/maxk_hip.h is the drop-in boundary for any FFI: it must compile as C99 on its
+    own (no C++, no HIP or torch types)."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    src = tmp_path / "use_header.c"
+    src.write_text('#include "maxk_hip.h"\n'
+                   "int main(void) {\n"
+                   "  maxk_plan_options o = {0};\n"
+                   "  maxk_plan_info i;\n"
+                   "  (void)o; (void)i;\n"
+                   "  return maxk_abi_version() == MAXK_ABI_VERSION ? 0 : 1;\n"
+                   "}\n")
+    r = subprocess.run([cc, "-std=c99", "-Wall", "-Werror", "-pedantic", "-fsyntax-only",
+                        "-I", os.path.dirname(HEADER), str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
