@@ -6,13 +6,16 @@
 // metadata is derived once from the CSR row pointer and the column indices and cached by
 // the caller:
 //
-//   forward : tasks of <= 16 whole rows with <= cap edges (heavy first); rows longer
+//   forward : tasks of <= 32 whole rows with <= cap edges (heavy first); rows longer
 //             than cap are split into segments whose outputs are pre-zeroed and summed
-//             with float atomics (the only atomics left in the forward).
+//             with float atomics (the only atomics left in the forward). Each task's edges
+//             are sorted by column (8-B words {column | row-in-task, val}) with window
+//             offsets for the clock-rotated sweep.
 //   backward: a stable radix sort of the edges by source-column block
 //             (hipcub::DeviceRadixSort, keys = idx / block_cols) gives the block-major,
-//             row-sorted edge list {row, col, val}; each block's range is cut into
-//             work-group tasks.
+//             row-sorted edge list, packed as 12-B records {row * D * 4, column in block,
+//             val}; each block's range is cut into row-chunk tasks (same row bounds in every
+//             block, XCD-aware order).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>

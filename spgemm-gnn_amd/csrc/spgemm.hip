@@ -12,16 +12,18 @@
 //
 //   forward : a 256-thread work-group owns <= 32 whole destination rows (LDS accumulator
 //             rows x D); its edges are processed flat, k/4 lanes per edge, 4 features per
-//             lane (one dwordx4 value gather + one dword selector gather), U independent
-//             sub-steps in flight per wave; products are accumulated in LDS with f64
-//             atomics (ds_add_f64, ~9x the f32 rate) or an f32 compare-and-swap loop, and
-//             the rows are written back once with coalesced dwordx4 stores. Only rows
-//             longer than the task cap are split, and only those touch global atomics.
+//             lane (one dwordx4 value gather + one dword selector gather; or lane chunks of
+//             3 values + their selectors for k % 16 != 0), U independent sub-steps in
+//             flight per wave; products are accumulated in LDS with f64 atomics
+//             (ds_add_f64, ~9x the f32 rate), and the rows are written back once with
+//             coalesced dwordx4 stores. Only rows longer than the task cap are split, and
+//             only those touch global atomics.
 //   backward: a 512-thread work-group owns a block of source columns whose k-wide
 //             gradients live in LDS; it sweeps the block's edges in destination-row order
 //             (plan-built block-major edge list), so the lanes of one instruction gather
-//             from few rows of grad_out (L1 reuse); the block is stored (or atomically
-//             flushed when it is split over several work-groups) once at the end.
+//             from few rows of grad_out (L1 reuse); updates are 64-bit compare-and-swaps on
+//             float pairs; the block is stored (or atomically flushed when it is split over
+//             several work-groups) once at the end.
 #include <algorithm>
 
 #include "common.h"
