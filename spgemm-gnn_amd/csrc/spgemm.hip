@@ -1075,6 +1075,18 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
                  (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0) |
                  (plan->fwd_quad && Lf % 4 == 0 && W == 4 ? kFwdFlagQuad : 0);
   if ((k % 4 == 0 || plan->fwd_chunk3) && plan->fwd_acc == MAXK_ACC_F64 &&
+      plan->fwd_unroll == 16 && W == 4) {
+    switch (FL & 7) {  // 16 sub-steps in flight per wave (no quad loads)
+      case 0: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 0); break;
+      case 1: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 1); break;
+      case 2: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 2); break;
+      case 3: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 3); break;
+      case 4: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 4); break;
+      case 5: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 5); break;
+      case 6: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 6); break;
+      default: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 7); break;
+    }
+  } else if ((k % 4 == 0 || plan->fwd_chunk3) && plan->fwd_acc == MAXK_ACC_F64 &&
       plan->fwd_unroll == 8) {
     if (FL & kFwdFlagQuad) FWD_LAUNCH_FLQ();
     else if (W == 8) FWD_LAUNCH_FL(512);
