@@ -32,6 +32,19 @@ constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k atomics) vs it
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
 constexpr double kFwdSlotEdgeRate = 1.6e8;  // edges/s one forward slot sustains at k = 16
+// two-pass backward below this many expected edges per (row, column block), i.e. when a
+// column block sees each grad_out row it fetches about once. Measured (blocks vs two-pass,
+// ms): ogbn-products k = 16 (0.04) 13.4 / 6.0, k = 32 (0.02) 16.0 / 8.3; yelp k = 64 (0.015)
+// 1.98 / 1.81; flickr k = 8 (0.50) 0.25 / 0.06; Reddit k = 64 (0.96) 4.86 / 15.2, k = 16 (3.8)
+// 1.70 / 5.35; ogbn-proteins k = 8 (15) 0.94 / 2.68
+constexpr double kBwdTwoPassReuse = 0.75;
+#if defined(MAXK_PROBE) && MAXK_PROBE == 13  // tools/ probe builds: other caps
+constexpr int kBwdRowsPerWave = 8;
+#elif defined(MAXK_PROBE) && MAXK_PROBE == 14
+constexpr int kBwdRowsPerWave = 1;
+#else
+constexpr int kBwdRowsPerWave = 4;  // row pass: most destination rows one wavefront stages
+#endif
 constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (S = 2, 4 measured slower)
 // Records past the end of the backward edge list that a wave may read (and ignore).
 constexpr int kBwdRecPad = (kBwdThreads / kWave) * kWave * 16 + kWave;  // MI355X: 8 XCDs, work-groups dealt round-robin (speed only)
@@ -178,5 +191,12 @@ struct maxk_plan {
   int32_t fwd_two_tables = 0;    // gather from sp_data / sp_index directly (no pack)
   int32_t bwd_csc = 0;           // column-major kernel (sparse graphs): one wave per column
   int32_t* bwd_colptr = nullptr; // [num_cols + 1] offsets of the column-sorted records
+  // two-pass backward (low row reuse): a row pass writes each edge's k products val *
+  // grad_out[r, sel(c)] into the edge's slot of bwd_tbuf (CSR order), a column pass sums the
+  // slots of each column's in-edges (bwd_perm, bwd_colptr)
+  int32_t bwd_twopass = 0;
+  int32_t bwd_tp_rows = 1;       // R: destination rows per wavefront of the row pass
+  uint32_t* bwd_erec = nullptr;  // [num_edges][2] CSR order: {column, val}
+  float* bwd_tbuf = nullptr;     // [num_edges][k] workspace
   int64_t device_bytes = 0;
 };

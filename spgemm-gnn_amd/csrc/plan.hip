@@ -176,6 +176,19 @@ __global__ void build_bwd_rec_kernel(const int32_t* __restrict__ perm,
   }
 }
 
+// Two-pass backward edge records in CSR order: {column | (row % R) << kFwdColBits, val}
+// (idx == nullptr: only the val field is refreshed).
+__global__ void build_erec_kernel(const int32_t* __restrict__ idx,
+                                  const int32_t* __restrict__ row_of, int R,
+                                  const float* __restrict__ val, int64_t E,
+                                  uint32_t* __restrict__ erec) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    if (idx) erec[2 * e] = (uint32_t)idx[e] | ((uint32_t)(row_of[e] % R) << kFwdColBits);
+    erec[2 * e + 1] = __float_as_uint(val ? val[e] : 1.0f);
+  }
+}
+
 static void dfree(void* q) { if (q) (void)hipFree(q); }
 
 static int grid_for(int64_t n, int threads) {
@@ -199,6 +212,8 @@ static void free_plan(maxk_plan* p) {
   dfree(p->bwd_rec);
   dfree(p->bwd_sel);
   dfree(p->bwd_colptr);
+  dfree(p->bwd_erec);
+  dfree(p->bwd_tbuf);
   delete p;
 }
 
@@ -298,8 +313,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                      (o.bwd_unroll == 0 || o.bwd_unroll == 4 || o.bwd_unroll == 8 ||
                       o.bwd_unroll == 12 || o.bwd_unroll == 16),
                  "maxk_plan_create: unroll must be 0, 8 or 16 (backward also 4 or 12)");
-  MAXK_CHECK_ARG(o.bwd_algo >= 0 && o.bwd_algo <= 2,
-                 "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks) or 2 (CSC)");
+  MAXK_CHECK_ARG(o.bwd_algo >= 0 && o.bwd_algo <= 3,
+                 "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks), 2 (CSC) or 3 "
+                 "(two-pass)");
   MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 2,
                  "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_sel_lds >= 0 && o.bwd_sel_lds <= 2,
@@ -594,11 +610,39 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   const bool csc_ok = E > 0 && k % p->bwd_feats == 0 && (Lc & (Lc - 1)) == 0 && Lc <= kWave &&
                       (uint64_t)N * (uint64_t)D * 4u <= 0xffffffffull;
   p->bwd_csc = csc_ok && o.bwd_algo == 2;
-  if (p->bwd_csc) {
+  // Two-pass backward (bwd_algo = 3; auto when a column block would see each grad_out row it
+  // fetches about once): a row pass stages grad_out[r] in LDS once per row and writes each
+  // edge's k products into its slot of an E x k workspace (CSR order), then a column pass
+  // gathers the slots of each column's in-edges and sums them. Trades 8k bytes of workspace
+  // traffic per edge for gathers that stop missing (ogbn-products k = 32: a block of 1023
+  // columns gets 0.02 edges per row it touches).
+  // Rows per wavefront of the row pass: enough that a wavefront has ~256 edges, at most
+  // kBwdRowsPerWave, so low-degree rows do not leave most of the 64/L edge slots idle
+  // (ogbn-products, 50 edges per row, k = 32: R = 1 8.65 ms, 4 8.67, 8 9.07 for both passes)
+  const int Lt = k / 4;
+  int R = 1;
+  while (R < kBwdRowsPerWave && (double)R * E / std::max(N, 1) < 256.0) R *= 2;
+  bool tp_fits = true;  // each wavefront's slots are addressed with 32-bit byte offsets
+  for (int r0 = 0; r0 < N && tp_fits; r0 += R)
+    tp_fits = (uint64_t)(hp[std::min(N, r0 + R)] - hp[r0]) * (uint64_t)k * 4u < 0x80000000ull;
+  const bool tp_ok = E > 0 && k % 4 == 0 && (Lt & (Lt - 1)) == 0 && Lt <= kWave && NC > 0 &&
+                     tp_fits;
+  bool twopass = tp_ok && o.bwd_algo == 3;
+  if (tp_ok && o.bwd_algo == 0) {
+    const double reuse = (double)E / std::max(N, 1) * (double)std::min(C, NC) / NC;
+    size_t free_b = 0, total_b = 0;
+    const bool fits = hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+                      (double)E * k * 4.0 < 0.5 * (double)free_b;
+    twopass = reuse < kBwdTwoPassReuse && fits;
+  }
+  p->bwd_twopass = twopass;
+  p->bwd_tp_rows = R;
+  if (p->bwd_csc || p->bwd_twopass) {
     C = 1;
     p->bwd_sel_lds = 0;
   }
-  const bool xcd_order = o.bwd_order == 0 && !p->bwd_csc;
+  const bool colsort = p->bwd_csc || p->bwd_twopass;
+  const bool xcd_order = o.bwd_order == 0 && !colsort;
   int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
   if (xcd_order && nblocks >= kXcds) {
     // a multiple of the XCD count, so every XCD owns the same number of column blocks; and
@@ -611,7 +655,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   }
   p->bwd_block_cols = C;
   p->n_bwd_blocks = nblocks;
-  std::vector<int64_t> offs(p->bwd_csc ? 1 : nblocks + 1, 0);
+  std::vector<int64_t> offs(colsort ? 1 : nblocks + 1, 0);
   if (E > 0) {
     if (!row_of) {
       PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
@@ -634,19 +678,27 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     PLAN_TRY(hipMalloc(&temp, temp_bytes));
     PLAN_TRY(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, ids_in,
                                                 p->bwd_perm, (int)E, 0, end_bit, s));
-    PLAN_TRY(hipMalloc(&p->bwd_row, sizeof(int32_t) * E));
-    PLAN_TRY(hipMalloc(&p->bwd_col, sizeof(int32_t) * E));
-    PLAN_TRY(hipMalloc(&p->bwd_val, sizeof(float) * E));
-    p->device_bytes += (int64_t)E * 16;
-    hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
-                       p->bwd_perm, row_of, idx, val, E, p->bwd_row, p->bwd_col, p->bwd_val);
+    if (p->bwd_twopass) {
+      PLAN_TRY(hipMalloc(&p->bwd_erec, sizeof(uint32_t) * 2 * (size_t)E));
+      PLAN_TRY(hipMalloc(&p->bwd_tbuf, sizeof(float) * (size_t)E * k));
+      p->device_bytes += (int64_t)E * 12 + (int64_t)E * k * 4;  // + bwd_perm
+      hipLaunchKernelGGL(build_erec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx,
+                         row_of, R, val, E, p->bwd_erec);
+    } else {
+      PLAN_TRY(hipMalloc(&p->bwd_row, sizeof(int32_t) * E));
+      PLAN_TRY(hipMalloc(&p->bwd_col, sizeof(int32_t) * E));
+      PLAN_TRY(hipMalloc(&p->bwd_val, sizeof(float) * E));
+      p->device_bytes += (int64_t)E * 16;
+      hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
+                         p->bwd_perm, row_of, idx, val, E, p->bwd_row, p->bwd_col, p->bwd_val);
+    }
     PLAN_TRY(hipMalloc(&d_offs, sizeof(int32_t) * (nblocks + 1)));
     hipLaunchKernelGGL(key_offsets_kernel, dim3(nblocks / 256 + 1), dim3(256), 0, s, keys_out,
                        E, nblocks, reinterpret_cast<int32_t*>(d_offs));
     PLAN_TRY(hipGetLastError());
     int bad = 0;
     PLAN_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
-    if (p->bwd_csc) {
+    if (colsort) {
       // column pointers of the column-sorted edge list stay on the device
       p->bwd_colptr = reinterpret_cast<int32_t*>(d_offs);
       d_offs = nullptr;
@@ -670,8 +722,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   const int64_t min_task_edges = o.bwd_min_task_edges > 0 ? o.bwd_min_task_edges : kBwdMinTaskEdges;
   std::vector<BwdTask> btasks;
   int nshared = 0;
-  if (p->bwd_csc) {
-    // no tasks: the column-major kernel runs one wave per column
+  if (colsort) {
+    // no tasks: the column-major kernels run one wave per column
   } else if (xcd_order && E > 0 && nblocks > 0) {
     // Row-chunk-major, XCD-aware order. Chunk j of every block covers the same rows
     // [R_j, R_j+1) (equal edge counts over the whole graph), so the work-groups that run
@@ -771,7 +823,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     p->device_bytes += sizeof(BwdTask) * btasks.size();
   }
   // packed backward path: records instead of the three parallel arrays
-  if (packed || p->bwd_csc) {
+  if (p->bwd_twopass) {
+    // CSR-order records; bwd_perm (column order -> CSR edge) stays for the column pass
+  } else if (packed || p->bwd_csc) {
     PLAN_TRY(hipMalloc(&p->bwd_rec, sizeof(uint32_t) * 3 * (size_t)(E + kBwdRecPad)));
     PLAN_TRY(hipMemsetAsync(p->bwd_rec + 3 * E, 0, sizeof(uint32_t) * 3 * kBwdRecPad, s));
     hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, nullptr,
@@ -803,7 +857,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
 extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* stream) {
   MAXK_CHECK_ARG(p != nullptr, "maxk_plan_refresh_values: plan is null");
   if (p->num_edges == 0) return MAXK_OK;
-  if (p->bwd_rec)
+  if (p->bwd_erec)
+    hipLaunchKernelGGL(build_erec_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
+                       (hipStream_t)stream, nullptr, nullptr, 1, val, p->num_edges, p->bwd_erec);
+  else if (p->bwd_rec)
     hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
                        (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
                        p->bwd_block_cols, p->dim_origin, p->bwd_rec);
@@ -833,7 +890,7 @@ extern "C" int maxk_plan_get_info(const maxk_plan* p, maxk_plan_info* info) {
   info->bwd_tasks = p->n_bwd_tasks;
   info->bwd_shared_blocks = p->n_bwd_shared;
   info->device_bytes = p->device_bytes;
-  info->bwd_algo = p->bwd_csc ? 2 : 1;
+  info->bwd_algo = p->bwd_twopass ? 3 : p->bwd_csc ? 2 : 1;
   return MAXK_OK;
 }
 

@@ -50,7 +50,9 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
 // updates; 3: backward ds_add_u32 of the f32 bits instead of the read + CAS; 4: backward
 // ds_add_f32 (correct sums, timing of the native LDS float atomic); 5: backward without LDS
 // updates; 6: backward gathers from grad_out row 0 only (L1 hits); 7: both 5 and 6;
-// 9: forward as two ds_add_u32 per element (a split fixed-point accumulator's LDS cost).
+// 9: forward as two ds_add_u32 per element (a split fixed-point accumulator's LDS cost);
+// two-pass row pass: 10 without the workspace stores, 11 without the selector gathers;
+// 13 / 14: at most 8 / 1 rows per row-pass wavefront (correct sums).
 #ifndef MAXK_PROBE
 #define MAXK_PROBE 0
 #endif
@@ -921,6 +923,146 @@ __global__ __launch_bounds__(256) void sspmm_bwd_csc_kernel(
   }
 }
 
+// Two-pass backward (plan->bwd_twopass), pass 1: one wavefront per R consecutive destination
+// rows stages their grad_out rows in its LDS once, then walks their (contiguous) edges 64/L
+// at a time (L = k/4 lanes per edge): lane q of an edge on column c reads the 4 selectors
+// sp_index[c][4q..4q+3] (one dword), multiplies the 4 staged features of the edge's row
+// (row % R from the edge record) by val and stores them as one float4 into the edge's slot
+// T[e][4q..] (CSR order: the slots of a wavefront are contiguous, the stores coalesce; in
+// column order the scattered 64-B stores ran at a quarter of the bandwidth). The only gathers
+// left on the texture path are the k selector bytes per edge; grad_out is read once.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U, int R>
+__global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
+    const int32_t* __restrict__ ptr, const uint32_t* __restrict__ erec,
+    const float* __restrict__ G, const uint8_t* __restrict__ sp_index, float* __restrict__ T,
+    int N, int D, int k) {
+  // R rows of kMaxDim floats per wavefront (any u8 selector stays inside the wave's rows)
+  __shared__ float grow[256 / kWave][R * kMaxDim];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int r0 = (blockIdx.x * (256 / kWave) + w) * R;
+  if (r0 >= N) return;
+  const int r1 = min(N, r0 + R);
+  const int e0 = __builtin_amdgcn_readfirstlane(ptr[r0]);
+  const int e1 = __builtin_amdgcn_readfirstlane(ptr[r1]);
+  if (e0 >= e1) return;
+  {
+    float x[R][kMaxDim / kWave];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const float* g = G + (size_t)min(r0 + j, N - 1) * D;
+#pragma unroll
+      for (int i = 0; i < kMaxDim / kWave; ++i) {
+        const int f = lane + i * kWave;
+        const float y = g[min(f, D - 1)];  // unconditional: all R rows' loads in flight
+        x[j][i] = f < D ? y : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int i = 0; i < kMaxDim / kWave; ++i) grow[w][j * kMaxDim + lane + i * kWave] = x[j][i];
+  }
+  // the rows are written and read by this wavefront only
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int L = k >> 2;  // power of two <= 64 (checked by the plan)
+  const int EPS = kWave / L;
+  const int slot = lane / L;
+  const int q = lane - slot * L;
+  const float* row = grow[w];
+  // branchless: idle slots load the row's last edge again and their stores fall outside the
+  // row's buffer range (dropped), so every load of a step is in flight together
+  const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
+      T + (size_t)e0 * k, (short)0, (int)((uint32_t)(e1 - e0) * (uint32_t)k * 4u), 0x00020000);
+  for (int base = e0; base < e1; base += EPS * U) {
+    uint32_t c[U];
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = min(base + u * EPS + slot, e1 - 1);
+      const uint2 cv = *reinterpret_cast<const uint2*>(erec + 2 * (size_t)e);
+      c[u] = cv.x;  // column | (row % R) << kFwdColBits
+      v[u] = __uint_as_float(cv.y);
+    }
+    uint32_t sw[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#if MAXK_PROBE == 11
+      sw[u] = (c[u] & 0xff) * 0x01010101u;
+#else
+      sw[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)(c[u] & kFwdColMask) * k + 4 * q);
+#endif
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * EPS + slot;
+      const uint32_t off = e < e1 ? ((uint32_t)(e - e0) * (uint32_t)k + 4u * q) * 4u : 0xfffffff0u;
+      const float* rw = row + (R > 1 ? (c[u] >> kFwdColBits) * kMaxDim : 0);
+      u32x4 o;
+      o.x = __float_as_uint(v[u] * rw[sw[u] & 0xffu]);
+      o.y = __float_as_uint(v[u] * rw[(sw[u] >> 8) & 0xffu]);
+      o.z = __float_as_uint(v[u] * rw[(sw[u] >> 16) & 0xffu]);
+      o.w = __float_as_uint(v[u] * rw[sw[u] >> 24]);
+      // nontemporal (aux = 2): the workspace is far larger than the caches (Reddit k = 16
+      // 5.58 -> 5.35 ms for both passes, ogbn-products k = 32 8.71 -> 8.56)
+#if MAXK_PROBE == 10
+      if (o.x == 0x12345u) __builtin_amdgcn_raw_buffer_store_b128(o, tr, off, 0, 2);
+#else
+      __builtin_amdgcn_raw_buffer_store_b128(o, tr, off, 0, 2);
+#endif
+    }
+  }
+}
+
+// Two-pass backward, pass 2: one wavefront per column c sums the slots of the column's
+// in-edges perm[colptr[c] .. colptr[c+1]) (64/L slots per step, float4 per lane), reduces
+// over the slots with shuffles and stores grad_sp[c] (every column written once: no memset,
+// no atomics).
+template <int U>
+__global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
+    const int32_t* __restrict__ colptr, const int32_t* __restrict__ perm,
+    const float* __restrict__ T, float* __restrict__ grad_sp, int ncols, int k) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int c = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
+  if (c >= ncols) return;
+  const int L = k >> 2;
+  const int EPS = kWave / L;
+  const int slot = lane / L;
+  const int q = lane - slot * L;
+  const int e0 = colptr[c], e1 = colptr[c + 1];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int base = e0; base < e1; base += EPS * U) {
+    int32_t pe[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) pe[u] = perm[min(base + u * EPS + slot, e1 - 1)];
+    float4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      // idle slots load a valid slot again and drop it (no branch around the loads)
+      const float4 x = *reinterpret_cast<const float4*>(T + (size_t)pe[u] * k + 4 * q);
+      const bool ok = base + u * EPS + slot < e1;
+      t[u] = make_float4(ok ? x.x : 0.f, ok ? x.y : 0.f, ok ? x.z : 0.f, ok ? x.w : 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc.x += t[u].x;
+      acc.y += t[u].y;
+      acc.z += t[u].z;
+      acc.w += t[u].w;
+    }
+  }
+  for (int m = L; m < kWave; m <<= 1) {
+    acc.x += __shfl_xor(acc.x, m, kWave);
+    acc.y += __shfl_xor(acc.y, m, kWave);
+    acc.z += __shfl_xor(acc.z, m, kWave);
+    acc.w += __shfl_xor(acc.w, m, kWave);
+  }
+  if (slot == 0) *reinterpret_cast<float4*>(grad_sp + (size_t)c * k + 4 * q) = acc;
+}
+
 // --------------------------------------------------------------------------------------
 // dense CSR SpMM comparator: one wavefront per destination row, 4 features per lane.
 // --------------------------------------------------------------------------------------
@@ -1136,6 +1278,25 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   if (N == 0) return MAXK_OK;
   MAXK_CHECK_ARG(grad_out && sp_index && grad_sp, "maxk_sspmm_backward: null pointer");
   hipStream_t s = (hipStream_t)stream;
+  if (plan->bwd_twopass) {
+    // the plan checked k % 4 == 0, k / 4 a power of two <= 64, E > 0, NC > 0
+    const int R = plan->bwd_tp_rows;
+    const dim3 rgrid((N + 4 * R - 1) / (4 * R));
+#define ROWS_LAUNCH(RR)                                                                   \
+    hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR>), rgrid, dim3(256), 0, s, ptr,       \
+                       plan->bwd_erec, grad_out, sp_index, plan->bwd_tbuf, N, D, k)
+    if (R >= 8) ROWS_LAUNCH(8);
+    else if (R == 4) ROWS_LAUNCH(4);
+    else if (R == 2) ROWS_LAUNCH(2);
+    else ROWS_LAUNCH(1);
+#undef ROWS_LAUNCH
+    MAXK_LAUNCH_CHECK("sspmm_bwd_rows launch");
+    hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4>), dim3((plan->num_cols + 3) / 4), dim3(256), 0,
+                       s, plan->bwd_colptr, plan->bwd_perm, plan->bwd_tbuf, grad_sp,
+                       plan->num_cols, k);
+    MAXK_LAUNCH_CHECK("sspmm_bwd_cols launch");
+    return MAXK_OK;
+  }
   if (plan->bwd_csc) {
     const int F = plan->bwd_feats;
     if (F == 4) {

@@ -220,6 +220,48 @@ def test_sspmm_backward_csc_vs_oracle(gpu, gname, k, feats):
     assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
 
 
+@pytest.mark.parametrize("gname", list(GRAPHS))
+@pytest.mark.parametrize("d,k", [(256, 4), (256, 8), (256, 16), (256, 32), (256, 64), (256, 128),
+                                 (256, 24), (100, 8), (64, 16), (256, 256)])
+def test_sspmm_backward_twopass_vs_oracle(gpu, gname, d, k):
+    """Two-pass backward (bwd_algo=3: row pass into the E x k workspace, column pass); k=24
+    (6 lanes per edge) and edgeless graphs fall back to the blocks."""
+    p, ix, v = GRAPHS[gname]()
+    n = p.size - 1
+    x = graphs.features(n, d, seed=k)
+    g = graphs.features(n, d, seed=k + 1)
+    _, oi = oracle.maxk(x.numpy(), k)
+    ref, mag = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k, options=dict(bwd_algo=3))
+    assert plan.info()["bwd_algo"] == (1 if k == 24 or ix.size == 0 else 3)
+    assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
+    val.mul_(-2.0)                        # refresh_values rewrites the CSR-order records
+    ref, mag = oracle.sspmm_backward(p, ix, v * -2.0, g.numpy(), oi, with_mag=True)
+    plan.refresh_values(val)
+    assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
+
+
+def test_sspmm_backward_auto_twopass_on_sparse_wide_graph(gpu):
+    """A graph whose column blocks would see each grad_out row about once (2 edges per row,
+    60k columns) gets the two-pass backward by default; the forced block kernel agrees."""
+    n, e, k, d = 60_000, 120_000, 16, 256
+    ptr, idx = graphs.synthetic_csr(n, e, seed=41)
+    p, ix = ptr.numpy(), idx.numpy()
+    v = np.random.RandomState(41).uniform(-1.0, 1.0, ix.size).astype(np.float32)
+    x = graphs.features(n, d, seed=42)
+    g = graphs.features(n, d, seed=43)
+    _, oi = oracle.maxk(x.numpy(), k)
+    ref, mag = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    dptr, didx, dval = graph_on(gpu, p, ix, v)
+    plan = mk.GraphPlan(dptr, didx, dval, n, ix.size, d, k)
+    assert plan.info()["bwd_algo"] == 3
+    assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
+    forced = mk.GraphPlan(dptr, didx, dval, n, ix.size, d, k, options=dict(bwd_algo=1))
+    assert forced.info()["bwd_algo"] == 1
+    assert_close(forced.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
+
+
 def test_plan_picks_up_value_changes(gpu):
     p, ix, v = GRAPHS["synthetic"]()
     n = p.size - 1
@@ -297,7 +339,7 @@ PLAN_OPTIONS = [
     dict(bwd_unroll=16), dict(bwd_slot_groups=2), dict(bwd_slot_groups=4),
     dict(bwd_lds_bytes=4096), dict(bwd_tasks_per_cu=1), dict(bwd_acc_pad=2), dict(bwd_sel_lds=2),
     dict(bwd_unroll=4), dict(bwd_unroll=12),
-    dict(bwd_algo=2), dict(bwd_algo=2, bwd_unroll=4),
+    dict(bwd_algo=2), dict(bwd_algo=2, bwd_unroll=4), dict(bwd_algo=3),
     dict(bwd_algo=2, bwd_features_per_lane=1), dict(bwd_algo=2, bwd_features_per_lane=1, bwd_unroll=16),
     # chunked blocks (atomic flush into a memset grad_sp), both task orders
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256),
@@ -349,7 +391,7 @@ def test_plan_options_rejected(gpu):
     ptr, idx, val = graph_on(gpu, p, ix, v)
     for bad in (dict(fwd_unroll=7), dict(bwd_order=3), dict(bwd_slot_groups=3),
                 dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3),
-                dict(bwd_algo=3), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
+                dict(bwd_algo=4), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
                 dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3),
                 dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3), dict(fwd_two_tables=3)):
         with pytest.raises(RuntimeError):
