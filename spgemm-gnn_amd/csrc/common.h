@@ -32,6 +32,10 @@ constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k atomics) vs it
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
 constexpr double kFwdSlotEdgeRate = 1.6e8;  // edges/s one forward slot sustains at k = 16
+// CBSR tables (5k bytes per column) above these sizes get packed one-line forward records
+// even where two tables would otherwise be used (plan.hip: k >= 32 / k < 32)
+constexpr double kFwdPackedTableBytes = 150e6;
+constexpr double kFwdPackedTableBytes16 = 32e6;
 // two-pass backward below this many expected edges per (row, column block), i.e. when a
 // column block sees each grad_out row it fetches about once. Measured (blocks vs two-pass,
 // ms): ogbn-products k = 16 (0.04) 13.4 / 6.0, k = 32 (0.02) 16.0 / 8.3; yelp k = 64 (0.015)

@@ -531,10 +531,18 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // Two tables (no record pack): Reddit k = 32 2.65 -> 2.53 ms, k = 64 4.98 -> 4.92 (k = 16:
   // 1.35 vs 1.39 packed); and where the per-call pack of all NC records costs more than it
   // saves, below ~128 edges per column (an 8-GPU row shard of Reddit at k = 16: 0.221 ->
-  // 0.207 ms)
+  // 0.207 ms). But on a large table, whose gathers mostly miss L2, the record's one line
+  // beats the two tables' two (values + selectors): at k = 16 from tens of MB (yelp, 57 MB:
+  // 0.645 -> 0.54 ms packed; ogbn-products, 196 MB: 4.84 -> 2.95; flickr 7 MB and the
+  // Reddit shard 19 MB stay faster with two tables), at k = 32 only from HBM-sized tables
+  // (ogbn-products 392 MB: 4.95 -> 4.77; yelp 115 MB: 0.67 two tables vs 0.73); never at
+  // k = 64 (ogbn-products 7.08 two tables vs 7.44)
+  const bool big_table = (double)std::max(NC, 1) * 5.0 * k >
+                         (k >= 32 ? kFwdPackedTableBytes : kFwdPackedTableBytes16);
   p->fwd_two_tables = !p->fwd_chunk3 && k % 4 == 0 &&
                       (o.fwd_two_tables == 1 ||
-                       (o.fwd_two_tables == 0 && (k >= 32 || E < 128ll * std::max(NC, 1))));
+                       (o.fwd_two_tables == 0 &&
+                        (k >= 64 || (!big_table && (k >= 32 || E < 128ll * std::max(NC, 1))))));
   if (p->fwd_two_tables) {
     // no workspace: the kernel gathers from sp_data / sp_index
   } else if (p->fwd_chunk3 && NC > 0) {
