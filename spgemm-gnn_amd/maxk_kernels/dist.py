@@ -113,14 +113,15 @@ class ShardedAggregation:
     """One rank's share of Y = A densify(sp) and of its SSpMM backward.
 
     ``fwd``/``bwd`` default to the gfx950 kernels through one rectangular GraphPlan per
-    column phase; tests on CPU (gloo) inject checker callables to exercise the partition,
-    the phase layout and the collectives.
+    column phase (``plan_options``: the same knobs as ``GraphPlan(options=...)``, e.g.
+    ``{"bwd_algo": 3}``); tests on CPU (gloo) inject checker callables to exercise the
+    partition, the phase layout and the collectives.
     """
 
     def __init__(self, part: RowPartition, rank: int, ptr: torch.Tensor, idx: torch.Tensor,
                  val: torch.Tensor, dim_origin: int, dim_k: int,
                  group: Optional[dist.ProcessGroup] = None, fwd: Optional[FwdFn] = None,
-                 bwd: Optional[BwdFn] = None):
+                 bwd: Optional[BwdFn] = None, plan_options: Optional[dict] = None):
         self.part, self.rank, self.group = part, rank, group
         self.dim_origin, self.dim_k = int(dim_origin), int(dim_k)
         self.r0, self.r1 = part.rows(rank)
@@ -142,7 +143,7 @@ class ShardedAggregation:
                 pp, pi, pv = part.phase_csr(self.ptr, self.idx, self.val, p)
                 self.plans.append(GraphPlan(pp, pi, pv, self.n_local, pi.numel(),
                                             self.dim_origin, self.dim_k,
-                                            num_cols=part.phase_cols))
+                                            num_cols=part.phase_cols, options=plan_options))
         self._fwd = fwd or (lambda p, d, i, out: self.plans[p].forward(
             d, i, out, accumulate=out is not None))
         self._bwd = bwd or (lambda p, g, i: self.plans[p].backward(

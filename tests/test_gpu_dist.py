@@ -26,11 +26,14 @@ def _graph(n=6000, e=150_000, seed=41):
     return p, i, graphs.sage_mean_values(p)
 
 
-@pytest.mark.parametrize("world,phases", [(2, 1), (3, 1), (8, 1), (2, 2), (8, 2), (3, 3)])
+@pytest.mark.parametrize("world,phases,opts", [(2, 1, None), (3, 1, None), (8, 1, None),
+                                               (2, 2, None), (8, 2, None), (3, 3, None),
+                                               (2, 1, {"bwd_algo": 3}), (8, 2, {"bwd_algo": 3})])
 @pytest.mark.parametrize("k", [16, 32])
-def test_emulated_partition_matches_oracle(gpu, world, phases, k):
+def test_emulated_partition_matches_oracle(gpu, world, phases, opts, k):
     """Every rank's per-phase rectangular plans (columns remapped into the phase-major
-    padded table) on one GPU; the all-gather / reduce-scatter done with tensor ops."""
+    padded table) on one GPU; the all-gather / reduce-scatter done with tensor ops; also
+    with the two-pass backward forced on every shard."""
     p, i, v = _graph()
     n, d = p.numel() - 1, 256
     x = graphs.features(n, d, seed=5)
@@ -58,7 +61,9 @@ def test_emulated_partition_matches_oracle(gpu, world, phases, k):
         out = torch.empty((b - a, d), device=gpu)
         for ph in range(phases):
             pp, pi, pv = part.phase_csr(lp, li, lv, ph)
-            plan = mk.GraphPlan(pp, pi, pv, b - a, pi.numel(), d, k, num_cols=nc)
+            plan = mk.GraphPlan(pp, pi, pv, b - a, pi.numel(), d, k, num_cols=nc, options=opts)
+            if opts and pi.numel() > 0:
+                assert plan.info()["bwd_algo"] == 3
             plan.forward(table_d[ph * nc:(ph + 1) * nc], table_i[ph * nc:(ph + 1) * nc], out,
                          accumulate=ph > 0)
             grad_table[ph * nc:(ph + 1) * nc] += plan.backward(                # reduce-scatter
@@ -99,8 +104,8 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("phases", [1, 2])
-def test_sharded_aggregation_rccl_world1(gpu, phases):
+@pytest.mark.parametrize("phases,opts", [(1, None), (2, None), (1, {"bwd_algo": 3})])
+def test_sharded_aggregation_rccl_world1(gpu, phases, opts):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
@@ -112,7 +117,7 @@ def test_sharded_aggregation_rccl_world1(gpu, phases):
         g = graphs.features(n, d, seed=8).to(gpu)
         sd, si = mk.maxk_forward(x, k, return_index=True)
         part = RowPartition(ptr, 1, phases=phases)
-        shard = ShardedAggregation(part, 0, ptr, idx, val, d, k)
+        shard = ShardedAggregation(part, 0, ptr, idx, val, d, k, plan_options=opts)
         y = shard.forward(sd, si)
         gs = shard.backward(g)
         y_ref, _ = mk.spgemm_forward(ptr, idx, val, sd, si, n, idx.numel(), k, d)
