@@ -13,6 +13,14 @@ namespace maxk {
 constexpr int kWave = 64;               // CDNA wavefront width (never 32)
 constexpr int kFwdTileRows = 32;        // default destination rows per forward work-group
 constexpr int kFwdMaxTileRows = 64;
+// forward LDS accumulator row stride D + kFwdRowPad elements: rows start on different banks,
+// so lanes of different edges with nearby selectors (sorted CBSR slots) spread over banks
+// (Reddit: k = 16 1.354 -> 1.341 ms, k = 32 2.500 -> 2.470, k = 8 0.898 -> 0.905)
+#if defined(MAXK_PROBE) && MAXK_PROBE == 18
+constexpr int kFwdRowPad = 0;
+#else
+constexpr int kFwdRowPad = 1;
+#endif
 // forward edge word: source column in the low kFwdColBits bits, row within the tile above
 constexpr int kFwdColBits = 26;
 constexpr uint32_t kFwdColMask = (1u << kFwdColBits) - 1;

@@ -185,7 +185,7 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
 #pragma unroll
     for (int u = 0; u < U; ++u) wn[u] = load_cv(min(base + u * EPS + slot, last));
   }
-  for (; base < e1; base += stride) {
+  for (; base < e1; base += stride) {  // D: the accumulator's row stride
     uint32_t cw[U];
     float v[U];
     bool ok[U];
@@ -286,12 +286,16 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
   const int n = nrows * D;
+  const int DS = D + kFwdRowPad;  // LDS row stride (elements)
   __syncthreads();  // the previous task's write-back has finished reading acc
   if ((phase > 0 || accum) && !split) {  // continue from the stored rows
     const float* src = out + (size_t)t.row0 * D;
-    for (int i = threadIdx.x; i < n; i += NT) acc[i] = T(src[i]);
+    for (int i = threadIdx.x; i < n; i += NT) {
+      const int r = i / D;
+      acc[r * DS + (i - r * D)] = T(src[i]);
+    }
   } else {
-    for (int i = threadIdx.x; i < n; i += NT) acc[i] = T(0);
+    for (int i = threadIdx.x; i < nrows * DS; i += NT) acc[i] = T(0);
   }
   __syncthreads();
 
@@ -314,12 +318,12 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     // lanes load a clamped (valid) edge and skip the update.
     if (emid >= 0) {
       fwd_edges4<U, A, FL>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, seltab, D, k);
+                           rec_bytes, seltab, DS, k);
       fwd_edges4<U, A, FL>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, seltab, D, k);
+                           rec_bytes, seltab, DS, k);
     } else {
       fwd_edges4<U, A, FL>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, seltab, D, k);
+                           rec_bytes, seltab, DS, k);
     }
   } else {
     for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
@@ -328,7 +332,7 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
         const uint2 w = cv[e];
         const uint32_t cwv = w.x;
         const float v = __uint_as_float(w.y);
-        T* arow = acc + (cwv >> kFwdColBits) * D;
+        T* arow = acc + (cwv >> kFwdColBits) * DS;
         const size_t rb = (size_t)(cwv & kFwdColMask) * k;
         for (int l = l0; l < k; l += L) A::add(arow + sp_index[rb + l], v * sp_data[rb + l]);
       }
@@ -337,7 +341,10 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   __syncthreads();
 
   float* dst = out + (size_t)t.row0 * D;
-  auto get = [&](int i) -> float { return (float)acc[i]; };
+  auto get = [&](int i) -> float {
+    const int r = i / D;
+    return (float)acc[r * DS + (i - r * D)];
+  };
   if (!split) {
     if ((D & 3) == 0) {
       for (int i = threadIdx.x * 4; i < n; i += NT * 4)
@@ -1091,7 +1098,7 @@ __global__ __launch_bounds__(256) void dense_spmm_kernel(
 size_t acc_bytes(int acc) { return acc == MAXK_ACC_F32_CAS ? sizeof(float) : sizeof(double); }
 
 size_t fwd_lds_bytes(int tile_rows, int D, int acc) {
-  return (size_t)tile_rows * D * acc_bytes(acc);
+  return (size_t)tile_rows * (D + kFwdRowPad) * acc_bytes(acc);
 }
 
 size_t bwd_lds_bytes(int block_cols, int k, int acc) {
