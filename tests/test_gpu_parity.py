@@ -262,6 +262,37 @@ def test_sspmm_backward_auto_twopass_on_sparse_wide_graph(gpu):
     assert_close(forced.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
 
 
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("k", [16, 32])
+def test_unsorted_rows_and_multi_edges(gpu, algo, k):
+    """CSR rows with shuffled column order and repeated (row, column) edges: every edge
+    counts once per occurrence in both directions, whatever the backward kernel."""
+    rs = np.random.RandomState(55)
+    p, ix, v = GRAPHS["synthetic"]()
+    ix = ix.copy()
+    for r in range(p.size - 1):                       # shuffle each row's columns
+        rs.shuffle(ix[p[r]:p[r + 1]])
+    rows = np.repeat(np.arange(p.size - 1), np.diff(p))
+    dup = rs.rand(ix.size) < 0.1                      # repeat ~10 % of the edges in their row
+    rows = np.concatenate([rows, rows[dup]])
+    cols = np.concatenate([ix, ix[dup]])
+    vals = np.concatenate([v, rs.uniform(-1, 1, dup.sum()).astype(np.float32)])
+    order = np.argsort(rows, kind="stable")
+    rows, cols, vals = rows[order], cols[order].astype(np.int32), vals[order]
+    n, d = p.size - 1, 256
+    p2 = np.zeros(n + 1, np.int32)
+    p2[1:] = np.cumsum(np.bincount(rows, minlength=n))
+    x = graphs.features(n, d, seed=56)
+    g = graphs.features(n, d, seed=57)
+    od, oi = oracle.maxk(x.numpy(), k)
+    ref_f, mag_f = oracle.spgemm_forward(p2, cols, vals, od, oi, d, with_mag=True)
+    ref_b, mag_b = oracle.sspmm_backward(p2, cols, vals, g.numpy(), oi, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p2, cols, vals)
+    plan = mk.GraphPlan(ptr, idx, val, n, cols.size, d, k, options=dict(bwd_algo=algo))
+    assert_close(plan.forward(to_dev(od, gpu), to_dev(oi, gpu)), ref_f, mag_f)
+    assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref_b, mag_b)
+
+
 def test_plan_picks_up_value_changes(gpu):
     p, ix, v = GRAPHS["synthetic"]()
     n = p.size - 1
