@@ -751,7 +751,24 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     const int64_t fl = ((int64_t)cus + (int64_t)nblocks * S - 1) / ((int64_t)nblocks * S);
     if (o.bwd_min_task_edges == 0 && nch64 < fl && E / ((int64_t)nblocks * fl) >= 16384)
       nch64 = std::min<int64_t>(chunks, fl);
-    const int nch = (int)std::max<int64_t>(1, nch64);
+    nch64 = std::max<int64_t>(1, nch64);
+    // One 512-thread work-group per CU: a task count just past a multiple of the CUs leaves
+    // the last round mostly idle (ogbn-proteins k = 32: 192 blocks x 3 chunks = 2.25 rounds,
+    // 2.37 ms; x 4 = 3 rounds, 1.82 ms). With the default knobs take the chunk count in
+    // [nch, nch + 2] whose tasks fill their rounds best, keeping >= 0.6 x the minimum task.
+    if (o.bwd_tasks_per_cu == 0 && o.bwd_min_task_edges == 0) {
+      auto fill = [&](int64_t c) {
+        const int64_t t = (int64_t)nblocks * S * c;
+        return (double)t / ((double)((t + cus - 1) / cus) * cus);
+      };
+      int64_t best = nch64;
+      for (int64_t c = nch64 + 1; c <= nch64 + 2; ++c) {
+        if ((double)E / ((double)nblocks * c) < 0.6 * kBwdMinTaskEdges) break;
+        if (fill(c) > fill(best) + 0.05) best = c;
+      }
+      nch64 = best;
+    }
+    const int nch = (int)nch64;
     std::vector<int32_t> rb(nch + 1);
     for (int j = 0; j <= nch; ++j) {
       const int64_t target = E * j / nch;
