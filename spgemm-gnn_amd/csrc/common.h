@@ -16,11 +16,7 @@ constexpr int kFwdMaxTileRows = 64;
 // forward LDS accumulator row stride D + kFwdRowPad elements: rows start on different banks,
 // so lanes of different edges with nearby selectors (sorted CBSR slots) spread over banks
 // (Reddit: k = 16 1.354 -> 1.341 ms, k = 32 2.500 -> 2.470, k = 8 0.898 -> 0.905)
-#if defined(MAXK_PROBE) && MAXK_PROBE == 18
-constexpr int kFwdRowPad = 0;
-#else
 constexpr int kFwdRowPad = 1;
-#endif
 // forward edge word: source column in the low kFwdColBits bits, row within the tile above
 constexpr int kFwdColBits = 26;
 constexpr uint32_t kFwdColMask = (1u << kFwdColBits) - 1;
@@ -50,13 +46,7 @@ constexpr double kFwdPackedTableBytes16 = 32e6;
 // 1.98 / 1.81; flickr k = 8 (0.50) 0.25 / 0.06; Reddit k = 64 (0.96) 4.86 / 15.2, k = 16 (3.8)
 // 1.70 / 5.35; ogbn-proteins k = 8 (15) 0.94 / 2.68
 constexpr double kBwdTwoPassReuse = 0.75;
-#if defined(MAXK_PROBE) && MAXK_PROBE == 13  // tools/ probe builds: other caps
-constexpr int kBwdRowsPerWave = 8;
-#elif defined(MAXK_PROBE) && MAXK_PROBE == 14
-constexpr int kBwdRowsPerWave = 1;
-#else
 constexpr int kBwdRowsPerWave = 4;  // row pass: most destination rows one wavefront stages
-#endif
 constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (S = 2, 4 measured slower)
 // Records past the end of the backward edge list that a wave may read (and ignore).
 constexpr int kBwdRecPad = (kBwdThreads / kWave) * kWave * 16 + kWave;  // MI355X: 8 XCDs, work-groups dealt round-robin (speed only)

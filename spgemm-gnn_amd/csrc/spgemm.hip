@@ -45,37 +45,12 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, W * 0x55, 0xf, 0xf, false);
 }
 
-// MAXK_PROBE (tools/ builds only, `make probe`; never in the product library): speed probes
-// with wrong numerics. 1: forward ds_add_u64 of the f64 bits; 2: forward without LDS
-// updates; 3: backward ds_add_u32 of the f32 bits instead of the read + CAS; 4: backward
-// ds_add_f32 (correct sums, timing of the native LDS float atomic); 5: backward without LDS
-// updates; 6: backward gathers from grad_out row 0 only (L1 hits); 7: both 5 and 6;
-// 9: forward as two ds_add_u32 per element (a split fixed-point accumulator's LDS cost);
-// two-pass row pass: 10 without the workspace stores, 11 without the selector gathers;
-// 13 / 14: at most 8 / 1 rows per row-pass wavefront (correct sums).
-#ifndef MAXK_PROBE
-#define MAXK_PROBE 0
-#endif
 
 template <>
 struct LdsAcc<MAXK_ACC_F64> {
   using T = double;
   static __device__ __forceinline__ void add(double* p, float v) {
-#if MAXK_PROBE == 1
-    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p),
-                           (unsigned long long)__double_as_longlong((double)v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-#elif MAXK_PROBE == 2
-    if (v == 1.2345e-30f) lds_add(p, (double)v);  // practically never: keeps the gathers live
-#elif MAXK_PROBE == 9
-    unsigned* u = reinterpret_cast<unsigned*>(p);
-    const int q = __float2int_rz(v * 32768.f);
-    __hip_atomic_fetch_add(u, (unsigned)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(u + 1, (unsigned)__float2int_rz(v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
     lds_add(p, (double)v);
-#endif
   }
 };
 
@@ -596,11 +571,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-#if MAXK_PROBE == 6 || MAXK_PROBE == 7
-        const uint32_t off = (((s[u] >> (8 * i)) & 0xffu) << 2);  // row 0 only: L1 hits
-#else
         const uint32_t off = go[u] + (((s[u] >> (8 * i)) & 0xffu) << 2);
-#endif
         x[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
       }
     }
@@ -615,34 +586,6 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[u][i] *= v[u];
-#if MAXK_PROBE == 5 || MAXK_PROBE == 7
-    {
-      float sink = 0.f;
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sink += x[u][i];
-      if (sink == 1.2345e-30f) accq[0] = 1u;  // practically never: keeps the gathers live
-    }
-    continue;
-#endif
-#if MAXK_PROBE == 3 || MAXK_PROBE == 4
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      unsigned* a = accq + cl[u] * KS;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (ok[u]) {
-          if (MAXK_PROBE == 3)
-            __hip_atomic_fetch_add(a + i * L, __float_as_uint(x[u][i]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-          else
-            __hip_atomic_fetch_add(reinterpret_cast<float*>(a + i * L), x[u][i],
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
-    continue;
-#endif
     if constexpr (V) {
       using u64 = unsigned long long;
       u64 old2[U][2];
@@ -998,11 +941,7 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
     uint32_t sw[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-#if MAXK_PROBE == 11
-      sw[u] = (c[u] & 0xff) * 0x01010101u;
-#else
       sw[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)(c[u] & kFwdColMask) * k + 4 * q);
-#endif
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = base + u * EPS + slot;
@@ -1015,11 +954,7 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
       o.w = __float_as_uint(v[u] * rw[sw[u] >> 24]);
       // nontemporal (aux = 2): the workspace is far larger than the caches (Reddit k = 16
       // 5.58 -> 5.35 ms for both passes, ogbn-products k = 32 8.71 -> 8.56)
-#if MAXK_PROBE == 10
-      if (o.x == 0x12345u) __builtin_amdgcn_raw_buffer_store_b128(o, tr, off, 0, 2);
-#else
       __builtin_amdgcn_raw_buffer_store_b128(o, tr, off, 0, 2);
-#endif
     }
   }
 }

@@ -41,9 +41,9 @@ def ref_compat_py(row, k):
     f = np.float32
     s = [f(v) for v in row]
     lo = hi = s[0]
-    for v in s[1:]:
-        lo = min(lo, v)
-        hi = max(hi, v)
+    for v in s[1:]:  # FMNMX: a NaN operand yields the other one (np.fmin / np.fmax)
+        lo = f(np.fmin(lo, v))
+        hi = f(np.fmax(hi, v))
     p = f(f(lo + hi) * f(0.5))
     for _ in range(8):
         cnt = sum(1 for v in s if v > p)
@@ -94,6 +94,39 @@ def test_ref_compat_matches_python_restatement(k):
     for r in range(x.shape[0]):
         pd, pi = ref_compat_py(x[r], k)
         assert np.array_equal(pd, d[r]) and np.array_equal(pi, i[r]), r
+
+
+EDGE = os.path.join(os.path.dirname(__file__), "golden", "maxk_refcompat_edge.npz")
+
+
+@pytest.mark.parametrize("k", [1, 8, 16, 32, 64])
+def test_ref_compat_edge_fixtures(k):
+    """NaN / +-Inf / +-0 / all-equal / cap-with-cnt>k / cap-with-cnt<k / denormal rows
+    (tests/golden/make_golden.py:edge_rows): the committed fixture, the C oracle and the
+    literal restatement agree bit for bit."""
+    with np.load(EDGE, allow_pickle=False) as z:
+        x, gd, gi = z["x"], z[f"data_k{k}"], z[f"index_k{k}"]
+    d, i = oracle.maxk(x, k, "ref_compat")
+    assert np.array_equal(i, gi) and np.array_equal(d.view(np.uint32), gd.view(np.uint32))
+    with np.errstate(invalid="ignore", over="ignore"):
+        for r in range(x.shape[0]):
+            pd, pi = ref_compat_py(x[r], k)
+            assert np.array_equal(pi, gi[r]), r
+            assert np.array_equal(pd.view(np.uint32), gd[r].view(np.uint32)), r
+
+
+def test_ref_compat_edge_fixtures_cover_the_cap_exits():
+    """The fixture holds a row ending the 8 steps with cnt > k (k slots filled from more
+    candidates) and one with cnt < k (padding (0.0f, 0) after the last hit)."""
+    with np.load(EDGE, allow_pickle=False) as z:
+        x, gi = z["x"], z["index_k16"]
+    k = 16
+    counts = []
+    for r in range(x.shape[0]):
+        pd, pi = ref_compat_py(x[r], k)
+        counts.append(int((pd != 0).sum()))
+    assert counts[10] == k and (x[10] > 0).sum() > k  # cnt > k at the cap
+    assert 0 < counts[11] < k                          # cnt < k at the cap
 
 
 @pytest.mark.parametrize("k", [8, 16, 24, 64])
