@@ -27,21 +27,31 @@ from .ops import (  # noqa: F401
 )
 from .autograd import (  # noqa: F401
     CSRGraph,
+    DenseAggFunction,
     MaxKFunction,
     SpGEMMFunction,
+    dense_aggregate,
     densify,
     maxk,
     maxk_aggregate,
     spgemm,
 )
 
-from .layers import MaxKGCN, MaxKGCNConv, MaxKSAGE, MaxKSAGEConv  # noqa: F401,E402
+from .layers import (  # noqa: F401,E402
+    MaxKGCN,
+    MaxKGCNConv,
+    MaxKGIN,
+    MaxKGINConv,
+    MaxKSAGE,
+    MaxKSAGEConv,
+)
 
 __all__ = [
     "maxk_forward", "maxk_backward", "spgemm_forward", "spgemm_backward",
     "dense_spmm", "GraphPlan", "get_plan", "clear_plan_cache", "CSRGraph",
     "MaxKFunction", "SpGEMMFunction", "maxk", "spgemm", "maxk_aggregate", "MaxKError",
-    "densify", "MaxKSAGEConv", "MaxKGCNConv", "MaxKSAGE", "MaxKGCN",
+    "densify", "MaxKSAGEConv", "MaxKGCNConv", "MaxKGINConv", "MaxKSAGE", "MaxKGCN",
+    "MaxKGIN", "dense_aggregate", "DenseAggFunction",
 ]
 
 ABI_VERSION = lib.maxk_abi_version()

@@ -127,6 +127,25 @@ class CSRGraph:
         self._values[kind] = v
         return v
 
+    def transposed(self) -> "CSRGraph":
+        """A^T with the same edge values (row = source node), cached: the backward of the
+        dense aggregation, dX = A^T dY, runs the same SpMM kernel on it."""
+        key = ("transposed", self.val.data_ptr(), self.val._version)
+        g = self._values.get(key)
+        if g is None:
+            rows = torch.repeat_interleave(torch.arange(self.num_nodes, device=self.device),
+                                           self.in_degrees())
+            cols = self.idx.to(torch.int64)
+            order = torch.argsort(cols * self.num_nodes + rows, stable=True)
+            cnt = torch.bincount(cols, minlength=self.num_nodes)
+            ptr = torch.zeros(self.num_nodes + 1, dtype=torch.int64, device=self.device)
+            ptr[1:] = torch.cumsum(cnt, 0)
+            g = CSRGraph(ptr, rows[order], self.val[order])
+            self._values = {k: v for k, v in self._values.items()
+                            if not (isinstance(k, tuple) and k[0] == "transposed")}
+            self._values[key] = g
+        return g
+
     def with_values(self, kind: str) -> "CSRGraph":
         """Same structure with the ``kind`` edge weights (shares ptr/idx, hence the plan)."""
         key = ("graph", kind)
@@ -180,6 +199,31 @@ class SpGEMMFunction(torch.autograd.Function):
                                           graph.num_edges, k, dim_origin,
                                           plan=graph.plan(dim_origin, k))
         return grad_sp, None, None, None
+
+
+class DenseAggFunction(torch.autograd.Function):
+    """Y = A X on dense features (DGL ``update_all(copy_u('h'), sum)`` with the graph's edge
+    values, i.e. mean / GraphConv normalisation through ``CSRGraph.with_values``): the
+    aggregation of the ReLU layers (utils/models.py:140,252 with ``--nonlinear relu``).
+    Forward and backward both run ``maxk_dense_spmm_csr``; the backward on A^T."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, graph: CSRGraph):
+        ctx.graph = graph
+        return ops.dense_spmm(graph.ptr, graph.idx, graph.val, x.contiguous())
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        grad_x = None
+        if ctx.needs_input_grad[0]:
+            gt = ctx.graph.transposed()
+            grad_x = ops.dense_spmm(gt.ptr, gt.idx, gt.val, grad_out.contiguous())
+        return grad_x, None
+
+
+def dense_aggregate(x: torch.Tensor, graph: CSRGraph) -> torch.Tensor:
+    """Y = A @ x for dense x (ReLU layers), differentiable in x."""
+    return DenseAggFunction.apply(x, graph)
 
 
 def densify(sp_data: torch.Tensor, sp_index: torch.Tensor, dim_origin: int) -> torch.Tensor:

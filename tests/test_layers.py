@@ -13,7 +13,8 @@ import torch
 
 import maxk_kernels as mk
 from maxk_kernels import graphs
-from maxk_kernels.layers import MaxKGCN, MaxKGCNConv, MaxKSAGE, MaxKSAGEConv
+from maxk_kernels.layers import (MaxKGCN, MaxKGCNConv, MaxKGIN, MaxKGINConv, MaxKSAGE,
+                                 MaxKSAGEConv)
 
 
 def small_edges(n=300, e=4000, seed=5):
@@ -50,6 +51,42 @@ def test_edge_values_match_dgl_norms():
     assert g.with_values("mean").ptr is g.ptr                       # plan shared
     with pytest.raises(ValueError):
         g.edge_values("max")
+
+
+def test_transposed_csr():
+    src = torch.tensor([0, 2, 1, 2, 3, 0])
+    dst = torch.tensor([1, 1, 0, 3, 3, 3])
+    g = mk.CSRGraph.from_edges(src, dst, 4).with_values("both")
+    t = g.transposed()
+    a = torch.sparse_csr_tensor(g.ptr.long(), g.idx.long(), g.val.double(), (4, 4)).to_dense()
+    at = torch.sparse_csr_tensor(t.ptr.long(), t.idx.long(), t.val.double(), (4, 4)).to_dense()
+    assert torch.equal(at, a.T)
+    assert g.transposed() is t                                     # cached
+
+
+def test_norm_class_or_instance_and_nonlinear_checks():
+    """utils/maxk_layers.py:66-67 passes norm as a class (norm(out_feats)); DGL passes an
+    instance; utils/config.py:47 allows nonlinear in {maxk, relu}."""
+    c1 = MaxKSAGEConv(8, 6, norm=torch.nn.LayerNorm)
+    assert isinstance(c1.norm, torch.nn.LayerNorm) and c1.norm.normalized_shape == (6,)
+    ln = torch.nn.LayerNorm(6)
+    assert MaxKSAGEConv(8, 6, norm=ln).norm is ln
+    for cls in (MaxKSAGE, MaxKGCN, MaxKGIN):
+        with pytest.raises(ValueError, match="nonlinear"):
+            cls(4, 8, 1, 2, 4, nonlinear="gelu")
+    with pytest.raises(ValueError):
+        MaxKSAGEConv(8, 8, nonlinear="tanh")
+
+
+@pytest.mark.parametrize("nonlinear", ["maxk", "relu"])
+@pytest.mark.parametrize("model", ["sage", "gcn", "gin"])
+def test_integrated_script_constructors(model, nonlinear):
+    """maxk_gnn_integrated.py:317-332 builds the three models positionally plus these
+    kwargs; the single import edit of INTEGRATION.md must keep all three names."""
+    from maxk_kernels import MaxKGCN as G, MaxKGIN as I, MaxKSAGE as S  # noqa: F401
+    cls = {"sage": MaxKSAGE, "gcn": MaxKGCN, "gin": MaxKGIN}[model]
+    m = cls(500, 64, 3, 7, 16, feat_drop=0.5, norm=True, nonlinear=nonlinear)
+    assert m.nonlinear == nonlinear and m.num_layers == 3
 
 
 # ------------------------------------------------------------------------ GPU helpers
@@ -158,7 +195,7 @@ def test_gcn_conv_zero_in_degree_check(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model_cls", [MaxKSAGE, MaxKGCN])
+@pytest.mark.parametrize("model_cls", [MaxKSAGE, MaxKGCN, MaxKGIN])
 def test_model_trains(gpu, model_cls):
     dst, src, n = small_edges(n=800, e=16000, seed=11)
     csr = mk.CSRGraph.from_edges(src.to(gpu), dst.to(gpu), n)
@@ -176,3 +213,120 @@ def test_model_trains(gpu, model_cls):
         losses.append(loss.item())
     assert np.isfinite(losses).all()
     assert losses[-1] < losses[0] - 0.1      # random labels: fitting, not generalising
+
+
+# ------------------------------------------------------------------------ ReLU / GIN paths
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [64, 256, 100])
+def test_dense_aggregate_matches_dense(gpu, d):
+    """DenseAggFunction (maxk_dense_spmm_csr forward, the same kernel on A^T backward)."""
+    dst, src, n = small_edges(seed=13)
+    csr = mk.CSRGraph.from_edges(src.to(gpu), dst.to(gpu), n).with_values("both")
+    x = graphs.features(n, d, seed=3).to(gpu).requires_grad_(True)
+    y = mk.dense_aggregate(x, csr)
+    w = graphs.features(n, d, seed=4).to(gpu)
+    (y * w).sum().backward()
+    xr = x.detach().cpu().double().requires_grad_(True)
+    yr = dense_adj(csr, "both") @ xr
+    (yr * w.cpu().double()).sum().backward()
+    assert close(y, yr, 1e-6) and close(x.grad, xr.grad, 1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [8, 16])
+@pytest.mark.parametrize("nonlinear", ["maxk", "relu"])
+def test_gin_conv_matches_dense(gpu, k, nonlinear):
+    """dglnn.GINConv(learn_eps=True): (1 + eps) x + sum_{u->v} x_u on MaxK (or dense) x."""
+    dst, src, n = small_edges(seed=17)
+    csr = mk.CSRGraph.from_edges(src.to(gpu), dst.to(gpu), n)
+    conv = MaxKGINConv(64, maxk=k, nonlinear=nonlinear).to(gpu)
+    with torch.no_grad():
+        conv.eps.fill_(0.3)
+    x = graphs.features(n, 64, seed=5).to(gpu).requires_grad_(True)
+    y = conv(csr, x)
+    w = graphs.features(n, 64, seed=6).to(gpu)
+    (y * w).sum().backward()
+    xr = x.detach().cpu().double().requires_grad_(True)
+    eps = conv.eps.detach().cpu().double().requires_grad_(True)
+    xm = maxk_dense(xr, k) if nonlinear == "maxk" else xr
+    yr = (1 + eps) * xm + dense_adj(csr, "sum") @ xm
+    (yr * w.cpu().double()).sum().backward()
+    assert close(y, yr) and close(x.grad, xr.grad) and close(conv.eps.grad, eps.grad)
+
+
+def _dense_model_forward(model, name, nonlinear, k, A, x):
+    """f64 restatement of utils/models.py SAGE / GCN / GIN forward (DGL semantics) with the
+    module's own parameters; eval mode (no dropout)."""
+    P = {n_: p.detach().cpu().double() for n_, p in model.named_parameters()}
+    lin = lambda h, pre: h @ P[pre + ".weight"].T + P[pre + ".bias"]  # noqa: E731
+    act = (lambda h: maxk_dense(h, k)) if nonlinear == "maxk" else torch.relu
+    ln = lambda h, pre: torch.nn.functional.layer_norm(  # noqa: E731
+        h, h.shape[-1:], P[pre + ".weight"], P[pre + ".bias"], 1e-5)
+    if name == "sage":
+        h = lin(x, "lin_in")
+        for i in range(model.num_layers):
+            h = act(h)
+            pre = f"layers.{i}"
+            h = (h @ P[pre + ".fc_self.weight"].T + (A["mean"] @ h) @ P[pre + ".fc_neigh.weight"].T
+                 + P[pre + ".bias"])
+            h = ln(h, pre + ".norm")
+        return lin(h, "lin_out")
+    h = torch.relu(lin(x, "lin_in"))
+    for i in range(model.num_layers):
+        h = act(lin(h, f"linlayers.{i}"))
+        if name == "gcn":
+            h = A["both"] @ h + P[f"gcnlayers.{i}.bias"]
+        else:
+            h = (1 + P[f"ginlayers.{i}.eps"]) * h + A["sum"] @ h
+        h = ln(h, f"normlayers.{i}")
+    return lin(h, "lin_out")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nonlinear", ["maxk", "relu"])
+@pytest.mark.parametrize("name", ["sage", "gcn", "gin"])
+def test_models_with_integrated_script_kwargs_match_dense(gpu, name, nonlinear):
+    """The three models built exactly as maxk_gnn_integrated.py:317-332 builds them
+    (positional in/hid/layers/out/maxk, feat_drop, norm, nonlinear), forward and input
+    gradient against the f64 dense restatement of utils/models.py."""
+    dst, src, n = small_edges(n=400, e=6000, seed=19)
+    csr = mk.CSRGraph.from_edges(src.to(gpu), dst.to(gpu), n)
+    torch.manual_seed(4)
+    cls = {"sage": MaxKSAGE, "gcn": MaxKGCN, "gin": MaxKGIN}[name]
+    k = 16
+    model = cls(48, 64, 2, 7, k, feat_drop=0.5, norm=True, nonlinear=nonlinear).to(gpu).eval()
+    with torch.no_grad():  # non-trivial LayerNorm / bias / eps parameters
+        for pn, p in model.named_parameters():
+            if pn.endswith("bias") or "norm" in pn or pn.endswith("eps"):
+                p.add_(torch.empty_like(p).uniform_(-0.2, 0.2))
+    x = graphs.features(n, 48, seed=21).to(gpu).requires_grad_(True)
+    y = model(csr, x)
+    w = graphs.features(n, 7, seed=22).to(gpu)
+    (y * w).sum().backward()
+    A = {kind: dense_adj(csr, kind) for kind in ("mean", "both", "sum")}
+    xr = x.detach().cpu().double().requires_grad_(True)
+    yr = _dense_model_forward(model, name, nonlinear, k, A, xr)
+    (yr * w.cpu().double()).sum().backward()
+    assert close(y, yr, 2e-5), float((y.detach().double().cpu() - yr).abs().max())
+    assert close(x.grad, xr.grad, 2e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model_cls", [MaxKSAGE, MaxKGCN, MaxKGIN])
+def test_relu_models_train(gpu, model_cls):
+    dst, src, n = small_edges(n=800, e=16000, seed=11)
+    csr = mk.CSRGraph.from_edges(src.to(gpu), dst.to(gpu), n)
+    torch.manual_seed(3)
+    feats = graphs.features(n, 32, seed=12).to(gpu)
+    labels = torch.randint(0, 5, (n,), generator=torch.Generator().manual_seed(1)).to(gpu)
+    model = model_cls(32, 64, 2, 5, 16, feat_drop=0.1, norm=True, nonlinear="relu").to(gpu)
+    opt = torch.optim.Adam(model.parameters(), lr=0.01)
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(model(csr, feats), labels)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert np.isfinite(losses).all()
+    assert losses[-1] < losses[0] - 0.1
