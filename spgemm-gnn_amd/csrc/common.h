@@ -201,4 +201,11 @@ struct maxk_plan {
   uint32_t* bwd_erec = nullptr;  // [num_edges][2] CSR order: {column, val}
   float* bwd_tbuf = nullptr;     // [num_edges][k] workspace
   int64_t device_bytes = 0;
+  // per-call scratch: the forward's packed CBSR records (fwd_rec) and the backward's
+  // selector words (bwd_sel) or two-pass product workspace (bwd_tbuf). external_ws: the
+  // plan allocates none of them and the *_ws entry points take the caller's buffer (the
+  // Python layer passes one from torch's caching allocator on the launch stream)
+  int32_t external_ws = 0;
+  int64_t fwd_ws_bytes = 0;
+  int64_t bwd_ws_bytes = 0;
 };

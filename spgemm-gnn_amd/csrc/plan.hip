@@ -303,15 +303,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   MAXK_CHECK_ARG(ptr != nullptr && (E == 0 || idx != nullptr), "maxk_plan_create: null pointer");
   hipStream_t s = (hipStream_t)stream;
 
-  maxk_plan* p = new maxk_plan();
-  p->num_nodes = N;
-  p->num_cols = NC;
-  p->num_edges = E;
-  p->dim_origin = D;
-  p->dim_k = k;
-  p->src_ptr = ptr;
-  p->src_idx = idx;
-  p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
   MAXK_CHECK_ARG((o.fwd_unroll == 0 || o.fwd_unroll == 8 || o.fwd_unroll == 16) &&
                      (o.bwd_unroll == 0 || o.bwd_unroll == 4 || o.bwd_unroll == 8 ||
                       o.bwd_unroll == 12 || o.bwd_unroll == 16),
@@ -334,8 +325,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   MAXK_CHECK_ARG(o.bwd_slot_groups >= 0 && o.bwd_slot_groups <= 64 &&
                      (o.bwd_slot_groups & (o.bwd_slot_groups - 1)) == 0,
                  "maxk_plan_create: bwd_slot_groups must be 0 or a power of two <= 64");
-  p->fwd_unroll = o.fwd_unroll ? o.fwd_unroll : kFwdUnroll;
-  p->bwd_unroll = o.bwd_unroll ? o.bwd_unroll : kBwdUnroll;
   MAXK_CHECK_ARG((o.fwd_waves == 0 || o.fwd_waves == 4 || o.fwd_waves == 6 || o.fwd_waves == 8) &&
                      (o.bwd_waves == 0 || o.bwd_waves == 8 || o.bwd_waves == 12 ||
                       o.bwd_waves == 16),
@@ -347,12 +336,31 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                      (o.fwd_record_bytes % 16 == 0 &&
                       (o.fwd_chunk3 == 1 || (o.fwd_record_bytes >= 5 * k && k % 4 == 0))),
                  "maxk_plan_create: fwd_record_bytes must be 0 or a multiple of 16 >= 5k");
+  MAXK_CHECK_ARG(o.fwd_chunk3 >= 0 && o.fwd_chunk3 <= 2, "maxk_plan_create: fwd_chunk3 must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.bwd_features_per_lane == 0 || o.bwd_features_per_lane == 1 ||
+                     (o.bwd_features_per_lane == 4 && k % 4 == 0),
+                 "maxk_plan_create: bwd_features_per_lane must be 0, 1 or 4 (k % 4 == 0)");
+  MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
+                 "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.external_workspace == 0 || o.external_workspace == 1,
+                 "maxk_plan_create: external_workspace must be 0 or 1");
+  maxk_plan* p = new maxk_plan();
+  p->external_ws = o.external_workspace;
+  p->num_nodes = N;
+  p->num_cols = NC;
+  p->num_edges = E;
+  p->dim_origin = D;
+  p->dim_k = k;
+  p->src_ptr = ptr;
+  p->src_idx = idx;
+  p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
+  p->fwd_unroll = o.fwd_unroll ? o.fwd_unroll : kFwdUnroll;
+  p->bwd_unroll = o.bwd_unroll ? o.bwd_unroll : kBwdUnroll;
   // defaults measured on the Reddit-shaped graph (tools/sweep.py, profiles/r01)
   p->fwd_waves = o.fwd_waves ? o.fwd_waves : kFwdWaves;
   p->bwd_waves = o.bwd_waves ? o.bwd_waves : (k >= 32 ? 12 : kBwdWaves);
   p->fwd_prefetch = o.fwd_prefetch == 1;
   p->bwd_prefetch = o.bwd_prefetch == 1;
-  MAXK_CHECK_ARG(o.fwd_chunk3 >= 0 && o.fwd_chunk3 <= 2, "maxk_plan_create: fwd_chunk3 must be 0, 1 or 2");
   // lane-chunk records by default where the 4-values-per-lane layout fits k badly (Reddit:
   // k = 8 0.95 vs 1.02 ms, k = 24 1.93 vs 2.09 ms; k = 16 / 32 / 64 are slower with chunks),
   // and for every k % 4 != 0 (the alternative is the 1-feature-per-lane kernel)
@@ -367,9 +375,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   }
   p->fwd_acc = o.fwd_accumulator ? o.fwd_accumulator : MAXK_ACC_F64;
   p->bwd_acc = o.bwd_accumulator ? o.bwd_accumulator : MAXK_ACC_F32_CAS;
-  MAXK_CHECK_ARG(o.bwd_features_per_lane == 0 || o.bwd_features_per_lane == 1 ||
-                     (o.bwd_features_per_lane == 4 && k % 4 == 0),
-                 "maxk_plan_create: bwd_features_per_lane must be 0, 1 or 4 (k % 4 == 0)");
   p->bwd_feats = o.bwd_features_per_lane ? o.bwd_features_per_lane
                                          : (k % 4 == 0 ? 4 : 1);
 
@@ -529,8 +534,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     p->device_bytes += sizeof(int32_t) * zrows.size();
   }
 
-  MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
-                 "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
   // Two tables (no record pack): Reddit k = 32 2.65 -> 2.53 ms, k = 64 4.98 -> 4.92 (k = 16:
   // 1.35 vs 1.39 packed); and where the per-call pack of all NC records costs more than it
   // saves, below ~128 edges per column (an 8-GPU row shard of Reddit at k = 16: 0.221 ->
@@ -556,12 +559,14 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     }
     p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes
                                           : (b <= 64 ? 64 : b <= 128 ? 128 : b);
-    PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)NC * p->fwd_rec_bytes));
-    p->device_bytes += (int64_t)NC * p->fwd_rec_bytes;
+    p->fwd_ws_bytes = (int64_t)NC * p->fwd_rec_bytes;
   } else if (k % 4 == 0 && NC > 0) {
     p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes : cbsr_record_bytes(k);
-    PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)NC * p->fwd_rec_bytes));
-    p->device_bytes += (int64_t)NC * p->fwd_rec_bytes;
+    p->fwd_ws_bytes = (int64_t)NC * p->fwd_rec_bytes;
+  }
+  if (p->fwd_ws_bytes > 0 && !p->external_ws) {  // plan-owned per-call pack buffer
+    PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)p->fwd_ws_bytes));
+    p->device_bytes += p->fwd_ws_bytes;
   }
 
   // ---------------- backward
@@ -691,8 +696,12 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                                                 p->bwd_perm, (int)E, 0, end_bit, s));
     if (p->bwd_twopass) {
       PLAN_TRY(hipMalloc(&p->bwd_erec, sizeof(uint32_t) * 2 * (size_t)E));
-      PLAN_TRY(hipMalloc(&p->bwd_tbuf, sizeof(float) * (size_t)E * k));
-      p->device_bytes += (int64_t)E * 12 + (int64_t)E * k * 4;  // + bwd_perm
+      p->bwd_ws_bytes = (int64_t)E * k * 4;  // the E x k product workspace
+      if (!p->external_ws) {
+        PLAN_TRY(hipMalloc(&p->bwd_tbuf, (size_t)p->bwd_ws_bytes));
+        p->device_bytes += p->bwd_ws_bytes;
+      }
+      p->device_bytes += (int64_t)E * 12;  // erec + bwd_perm
       hipLaunchKernelGGL(build_erec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx,
                          row_of, R, val, E, p->bwd_erec);
     } else {
@@ -859,15 +868,18 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, nullptr,
                        p->bwd_row, p->bwd_col, p->bwd_val, E, C, D, p->bwd_rec);
     PLAN_TRY(hipGetLastError());
-    if (p->bwd_feats == 4)  // per-call lane-ordered selector words (pack_sel_kernel)
-      PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)std::max(NC, 1) * k));
+    if (p->bwd_feats == 4) {  // per-call lane-ordered selector words (pack_sel_kernel)
+      p->bwd_ws_bytes = (int64_t)std::max(NC, 1) * k;
+      if (!p->external_ws) PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)p->bwd_ws_bytes));
+    }
     PLAN_TRY(hipStreamSynchronize(s));
     dfree(p->bwd_row);
     dfree(p->bwd_col);
     dfree(p->bwd_val);
     p->bwd_row = p->bwd_col = nullptr;
     p->bwd_val = nullptr;
-    p->device_bytes += (p->bwd_feats == 4 ? (int64_t)NC * k : 0) + 12ll * kBwdRecPad;
+    p->device_bytes += (p->bwd_feats == 4 && !p->external_ws ? p->bwd_ws_bytes : 0) +
+                       12ll * kBwdRecPad;
   }
   PLAN_TRY(hipStreamSynchronize(s));
   dfree(row_of);
@@ -919,6 +931,14 @@ extern "C" int maxk_plan_get_info(const maxk_plan* p, maxk_plan_info* info) {
   info->bwd_shared_blocks = p->n_bwd_shared;
   info->device_bytes = p->device_bytes;
   info->bwd_algo = p->bwd_twopass ? 3 : p->bwd_csc ? 2 : 1;
+  return MAXK_OK;
+}
+
+extern "C" int maxk_plan_workspace_bytes(const maxk_plan* p, int64_t* fwd_bytes,
+                                         int64_t* bwd_bytes) {
+  MAXK_CHECK_ARG(p != nullptr, "maxk_plan_workspace_bytes: plan is null");
+  if (fwd_bytes) *fwd_bytes = p->fwd_ws_bytes;
+  if (bwd_bytes) *bwd_bytes = p->bwd_ws_bytes;
   return MAXK_OK;
 }
 

@@ -1093,7 +1093,7 @@ static int check_plan(const maxk_plan* plan, const int32_t* ptr, const int32_t* 
 static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const int32_t* idx,
                                const float* val, const float* sp_data, const uint8_t* sp_index,
                                float* out, int32_t N, int64_t E, int32_t k, int32_t D,
-                               void* stream, int accum) {
+                               void* stream, int accum, void* ws, int64_t ws_bytes) {
   MAXK_CHECK_ARG(N >= 0 && E >= 0, "maxk_spgemm_forward: negative size");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_spgemm_forward: dim_origin must be in [1, 256]");
   MAXK_CHECK_ARG(k >= 1 && k <= D, "k must be between 1 and input dimension");
@@ -1103,6 +1103,15 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   MAXK_CHECK_ARG(out && sp_data && sp_index && (E == 0 || (idx && val)) && ptr,
                  "maxk_spgemm_forward: null pointer");
   (void)val;  // the plan holds the permuted snapshot of (idx, val)
+  uint8_t* rec_ws = plan->fwd_rec;  // per-call pack of the CBSR records
+  if (ws) {
+    MAXK_CHECK_ARG(ws_bytes >= plan->fwd_ws_bytes,
+                   "maxk_spgemm_forward: workspace smaller than maxk_plan_workspace_bytes");
+    rec_ws = static_cast<uint8_t*>(ws);
+  } else if (plan->fwd_ws_bytes > 0 && !rec_ws) {
+    set_error("maxk_spgemm_forward: the plan has an external workspace; use maxk_spgemm_forward_ws");
+    return MAXK_ERR_INVALID_ARG;
+  }
   hipStream_t s = (hipStream_t)stream;
   if (plan->n_zero_rows > 0 && !accum) {  // split rows are summed atomically into zeroed rows
     hipLaunchKernelGGL(zero_rows_kernel, dim3(plan->n_zero_rows), dim3(256), 0, s,
@@ -1116,7 +1125,7 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   // two tables: values read straight from sp_data (4k-byte rows), selectors from sp_index
   const bool two = plan->fwd_two_tables;  // the plan only sets it with k % 4 == 0, no chunks
   const uint8_t* seltab = two ? sp_index : nullptr;
-  const uint8_t* recp = two ? reinterpret_cast<const uint8_t*>(sp_data) : plan->fwd_rec;
+  const uint8_t* recp = two ? reinterpret_cast<const uint8_t*>(sp_data) : rec_ws;
   const int rec_bytes_eff = two ? 4 * k : rec_bytes;
   if (two) {
     // nothing to pack
@@ -1124,13 +1133,13 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     const int64_t items = (int64_t)plan->num_cols * ((k + 2) / 3);
     const int grid = (int)std::min<int64_t>((items + 255) / 256, 65536);
     hipLaunchKernelGGL(pack_cbsr3_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
-                       plan->fwd_rec, plan->num_cols, k, rec_bytes);
+                       rec_ws, plan->num_cols, k, rec_bytes);
     MAXK_LAUNCH_CHECK("pack_cbsr3 launch");
   } else if (k % 4 == 0 && plan->num_cols > 0) {
     const int64_t words = (int64_t)plan->num_cols * (k + k / 4);
     const int grid = (int)std::min<int64_t>((words + 255) / 256, 65536);
     hipLaunchKernelGGL(pack_cbsr_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
-                       plan->fwd_rec, plan->num_cols, k, rec_bytes);
+                       rec_ws, plan->num_cols, k, rec_bytes);
     MAXK_LAUNCH_CHECK("pack_cbsr launch");
   }
   const int rot = plan->fwd_rot_ticks;
@@ -1224,7 +1233,20 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
                                    const int32_t* idx, const float* val,
                                    const float* sp_data, const uint8_t* sp_index, float* out,
                                    int32_t N, int64_t E, int32_t k, int32_t D, void* stream) {
-  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream, 0);
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream, 0,
+                             nullptr, 0);
+}
+
+extern "C" int maxk_spgemm_forward_ws(const maxk_plan* plan, const int32_t* ptr,
+                                      const int32_t* idx, const float* val,
+                                      const float* sp_data, const uint8_t* sp_index, float* out,
+                                      int32_t N, int64_t E, int32_t k, int32_t D,
+                                      int32_t accumulate, void* workspace,
+                                      int64_t workspace_bytes, void* stream) {
+  MAXK_CHECK_ARG(accumulate == 0 || accumulate == 1,
+                 "maxk_spgemm_forward_ws: accumulate must be 0 or 1");
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream,
+                             accumulate, workspace, workspace_bytes);
 }
 
 extern "C" int maxk_spgemm_forward_acc(const maxk_plan* plan, const int32_t* ptr,
@@ -1232,14 +1254,14 @@ extern "C" int maxk_spgemm_forward_acc(const maxk_plan* plan, const int32_t* ptr
                                        const float* sp_data, const uint8_t* sp_index,
                                        float* out, int32_t N, int64_t E, int32_t k, int32_t D,
                                        void* stream) {
-  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream, 1);
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream, 1,
+                             nullptr, 0);
 }
 
-extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
-                                   const int32_t* idx, const float* val,
-                                   const float* grad_out, const uint8_t* sp_index,
-                                   float* grad_sp, int32_t N, int64_t E, int32_t k, int32_t D,
-                                   void* stream) {
+static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const int32_t* idx,
+                               const float* val, const float* grad_out,
+                               const uint8_t* sp_index, float* grad_sp, int32_t N, int64_t E,
+                               int32_t k, int32_t D, void* stream, void* ws, int64_t ws_bytes) {
   (void)val;  // the plan holds the block-major snapshot of val
   MAXK_CHECK_ARG(N >= 0 && E >= 0, "maxk_sspmm_backward: negative size");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_sspmm_backward: dim_origin must be in [1, 256]");
@@ -1248,6 +1270,18 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
   if (rc) return rc;
   if (N == 0) return MAXK_OK;
   MAXK_CHECK_ARG(grad_out && sp_index && grad_sp, "maxk_sspmm_backward: null pointer");
+  // per-call scratch: selector words (column kernels) or the E x k products (two-pass)
+  uint32_t* sel_ws = plan->bwd_sel;
+  float* tbuf_ws = plan->bwd_tbuf;
+  if (ws) {
+    MAXK_CHECK_ARG(ws_bytes >= plan->bwd_ws_bytes,
+                   "maxk_sspmm_backward: workspace smaller than maxk_plan_workspace_bytes");
+    sel_ws = static_cast<uint32_t*>(ws);
+    tbuf_ws = static_cast<float*>(ws);
+  } else if (plan->bwd_ws_bytes > 0 && !sel_ws && !tbuf_ws) {
+    set_error("maxk_sspmm_backward: the plan has an external workspace; use maxk_sspmm_backward_ws");
+    return MAXK_ERR_INVALID_ARG;
+  }
   hipStream_t s = (hipStream_t)stream;
   if (plan->bwd_twopass) {
     // the plan checked k % 4 == 0, k / 4 a power of two <= 64, E > 0, NC > 0
@@ -1255,7 +1289,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     const dim3 rgrid((N + 4 * R - 1) / (4 * R));
 #define ROWS_LAUNCH(RR)                                                                   \
     hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR>), rgrid, dim3(256), 0, s, ptr,       \
-                       plan->bwd_erec, grad_out, sp_index, plan->bwd_tbuf, N, D, k)
+                       plan->bwd_erec, grad_out, sp_index, tbuf_ws, N, D, k)
     if (R >= 8) ROWS_LAUNCH(8);
     else if (R == 4) ROWS_LAUNCH(4);
     else if (R == 2) ROWS_LAUNCH(2);
@@ -1263,7 +1297,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
 #undef ROWS_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd_rows launch");
     hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4>), dim3((plan->num_cols + 3) / 4), dim3(256), 0,
-                       s, plan->bwd_colptr, plan->bwd_perm, plan->bwd_tbuf, grad_sp,
+                       s, plan->bwd_colptr, plan->bwd_perm, tbuf_ws, grad_sp,
                        plan->num_cols, k);
     MAXK_LAUNCH_CHECK("sspmm_bwd_cols launch");
     return MAXK_OK;
@@ -1273,13 +1307,13 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     if (F == 4) {
       const int nsel = plan->num_cols * (k / 4);
       hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
-                         plan->num_cols, k, 1, plan->bwd_sel);
+                         plan->num_cols, k, 1, sel_ws);
     }
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
     const dim3 cgrid((plan->num_cols + 3) / 4);
 #define CSC_LAUNCH(FF, UU)                                                                \
     hipLaunchKernelGGL((sspmm_bwd_csc_kernel<FF, UU>), cgrid, dim3(256), 0, s,            \
-                       plan->bwd_colptr, plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, \
+                       plan->bwd_colptr, plan->bwd_rec, grad_out, g_bytes, sel_ws, \
                        sp_index, grad_sp, plan->num_cols, k)
     if (F == 4) {
       if (plan->bwd_unroll >= 8) CSC_LAUNCH(4, 8);
@@ -1325,7 +1359,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     const int S = plan->bwd_slot_groups;
     const int nsel = plan->num_cols * (k / 4);
     hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
-                       plan->num_cols, k, S, plan->bwd_sel);
+                       plan->num_cols, k, S, sel_ws);
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
     const size_t lds4 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
                         (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
@@ -1333,7 +1367,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
     do {                                                                                  \
       if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, PF, V, Q>, lds4)); \
       hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF, V, Q>), grid, dim3(NT), lds4, s,  \
-                         plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, plan->bwd_sel, \
+                         plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sel_ws, \
                          grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds); \
     } while (0)
     const int W = plan->bwd_waves, U = plan->bwd_unroll;
@@ -1397,6 +1431,25 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
 #undef BWD_LAUNCH1
   MAXK_LAUNCH_CHECK("sspmm_bwd launch");
   return MAXK_OK;
+}
+
+extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
+                                   const int32_t* idx, const float* val,
+                                   const float* grad_out, const uint8_t* sp_index,
+                                   float* grad_sp, int32_t N, int64_t E, int32_t k, int32_t D,
+                                   void* stream) {
+  return sspmm_backward_impl(plan, ptr, idx, val, grad_out, sp_index, grad_sp, N, E, k, D,
+                             stream, nullptr, 0);
+}
+
+extern "C" int maxk_sspmm_backward_ws(const maxk_plan* plan, const int32_t* ptr,
+                                      const int32_t* idx, const float* val,
+                                      const float* grad_out, const uint8_t* sp_index,
+                                      float* grad_sp, int32_t N, int64_t E, int32_t k,
+                                      int32_t D, void* workspace, int64_t workspace_bytes,
+                                      void* stream) {
+  return sspmm_backward_impl(plan, ptr, idx, val, grad_out, sp_index, grad_sp, N, E, k, D,
+                             stream, workspace, workspace_bytes);
 }
 
 extern "C" int maxk_dense_spmm_csr(const int32_t* ptr, const int32_t* idx, const float* val,

@@ -24,6 +24,7 @@ SIGNATURES = {
     "maxk_abi_version": (ctypes.c_int, []),
     "maxk_last_error": (ctypes.c_char_p, []),
     "maxk_topk_cbsr": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
+    "maxk_topk_cbsr_count": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "maxk_scatter_backward": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "maxk_plan_create": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp,
                                         ctypes.POINTER(_vp)]),
@@ -40,6 +41,12 @@ SIGNATURES = {
                                                _i32, _i32, _vp]),
     "maxk_sspmm_backward": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
                                            _i32, _i32, _vp]),
+    "maxk_spgemm_forward_ws": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
+                                              _i32, _i32, _i32, _vp, _i64, _vp]),
+    "maxk_sspmm_backward_ws": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
+                                              _i32, _i32, _vp, _i64, _vp]),
+    "maxk_plan_workspace_bytes": (ctypes.c_int, [_vp, ctypes.POINTER(_i64),
+                                                 ctypes.POINTER(_i64)]),
     "maxk_dense_spmm_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),
     "maxk_warp4_build": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
 }
@@ -79,6 +86,7 @@ class PlanOptions(ctypes.Structure):
         ("fwd_two_tables", _i32),
         ("fwd_rot_windows", _i32),
         ("fwd_rot_rate", _i32),
+        ("external_workspace", _i32),
     ]
 
 

@@ -157,19 +157,43 @@ class CSRGraph:
 
 
 class MaxKFunction(torch.autograd.Function):
+    """x [N, D] -> CBSR (sp_data, sp_index); backward = the device scatter of grad_data
+    into the selected features (the ``grad * mask`` of utils/models.py:23-26).
+
+    ref_compat mode can fill fewer than k slots; the reference pads them with (0.0f, 0)
+    (SURVEY §8 a1). Those slots pass no gradient: before the scatter (last slot wins) each
+    padding slot is pointed at the row's last filled slot with that slot's gradient, so a
+    padding slot never writes (A^T G)[c, 0] into a feature 0 that was not selected."""
+
     @staticmethod
     def forward(ctx, x: torch.Tensor, k: int, mode: str = "exact"):
         x = x.contiguous()
-        sp_data, sp_index = ops.maxk_forward(x, k, mode=mode, return_index=True)
-        ctx.save_for_backward(sp_index)
+        if mode == "exact":
+            sp_data, sp_index = ops.maxk_forward(x, k, mode=mode, return_index=True)
+            ctx.save_for_backward(sp_index)
+        else:
+            sp_data, sp_index, count = ops.maxk_forward(x, k, mode=mode, return_index=True,
+                                                        return_count=True)
+            ctx.save_for_backward(sp_index, count)
         ctx.dim_origin = x.shape[1]
         ctx.mark_non_differentiable(sp_index)
         return sp_data, sp_index
 
     @staticmethod
     def backward(ctx, grad_data, grad_index):
-        (sp_index,) = ctx.saved_tensors
-        grad_x = ops.maxk_backward(grad_data.contiguous(), sp_index, dim_origin=ctx.dim_origin)
+        saved = ctx.saved_tensors
+        sp_index = saved[0]
+        grad_data = grad_data.contiguous()
+        if len(saved) == 2:
+            count = saved[1].to(torch.int64)
+            k = sp_index.shape[1]
+            pad = torch.arange(k, device=count.device)[None, :] >= count[:, None]
+            last = (count - 1).clamp(min=0)[:, None]
+            g_last = torch.where(count[:, None] > 0, grad_data.gather(1, last),
+                                 torch.zeros_like(grad_data[:, :1]))
+            sp_index = torch.where(pad, sp_index.gather(1, last), sp_index).contiguous()
+            grad_data = torch.where(pad, g_last, grad_data).contiguous()
+        grad_x = ops.maxk_backward(grad_data, sp_index, dim_origin=ctx.dim_origin)
         return grad_x, None, None
 
 
@@ -184,6 +208,7 @@ class SpGEMMFunction(torch.autograd.Function):
                                     dim_origin, plan=plan)
         ctx.save_for_backward(sp_index)
         ctx.graph = graph
+        ctx.plan = plan  # the backward uses the same plan (no cache lookup, no rebuild)
         ctx.dims = (dim_origin, k)
         return out
 
@@ -196,8 +221,7 @@ class SpGEMMFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             grad_sp = ops.spgemm_backward(graph.ptr, graph.idx, graph.val,
                                           grad_out.contiguous(), sp_index, graph.num_nodes,
-                                          graph.num_edges, k, dim_origin,
-                                          plan=graph.plan(dim_origin, k))
+                                          graph.num_edges, k, dim_origin, plan=ctx.plan)
         return grad_sp, None, None, None
 
 

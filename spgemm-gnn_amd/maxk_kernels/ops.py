@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import collections
 import ctypes
+import os
 import threading
 from typing import Optional, Tuple
 
@@ -53,7 +54,7 @@ def _check_tensor(t: torch.Tensor, name: str, dtype: Optional[torch.dtype] = Non
 # MaxK top-k
 # -------------------------------------------------------------------------------------
 def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
-                 return_index: bool = False, out=None):
+                 return_index: bool = False, out=None, return_count: bool = False):
     """MaxK nonlinearity -> CBSR. Reference: ``maxk_forward(input, k) -> [N, k] f32``.
 
     Checks (bindings.cpp:27-30): "input must be a CUDA tensor", "input must be
@@ -62,7 +63,9 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
     the reference kernel's 8-step bisection, bit-exact. With ``return_index=True`` returns
     ``(sp_data, sp_index)`` with ``sp_index`` u8 ``[N, k]`` in ascending feature order.
     ``out=(sp_data, sp_index)`` writes into caller-owned contiguous ``[N, k]`` tensors (e.g.
-    the send buffers of :class:`maxk_kernels.dist.ShardedAggregation`).
+    the send buffers of :class:`maxk_kernels.dist.ShardedAggregation`). ``return_count=True``
+    appends the int32 ``[N]`` number of filled slots per row (``k`` in exact mode; in
+    ref_compat mode the slots past it are the reference's ``(0.0f, 0)`` padding).
     """
     _need(input.is_cuda, "input must be a CUDA tensor")
     _need(input.is_contiguous(), "input must be contiguous")
@@ -83,10 +86,14 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
         _need(sp_index.shape == (n, k) and sp_index.dtype == torch.uint8 and
               sp_index.is_contiguous() and sp_index.device == input.device,
               "out[1] must be a contiguous uint8 [N, k] tensor on the input's device")
+    count = torch.empty(n, dtype=torch.int32, device=input.device) if return_count else None
     with torch.cuda.device(input.device):
-        check(lib.maxk_topk_cbsr(_p(input), _p(sp_data), _p(sp_index), n, d, k,
-                                 TOPK_MODES[mode], _stream()), "maxk_forward")
-    return (sp_data, sp_index) if return_index else sp_data
+        check(lib.maxk_topk_cbsr_count(_p(input), _p(sp_data), _p(sp_index), _p(count), n, d,
+                                       k, TOPK_MODES[mode], _stream()), "maxk_forward")
+    res = (sp_data, sp_index) if return_index else (sp_data,)
+    if return_count:
+        res = res + (count,)
+    return res if len(res) > 1 else res[0]
 
 
 def maxk_backward(grad_output: torch.Tensor, indices: torch.Tensor,
@@ -124,7 +131,14 @@ def maxk_backward(grad_output: torch.Tensor, indices: torch.Tensor,
 # graph plans (cached partition metadata)
 # -------------------------------------------------------------------------------------
 class GraphPlan:
-    """Owns one ``maxk_plan`` (device partition metadata for a CSR graph, k and D)."""
+    """Owns one ``maxk_plan`` (device partition metadata for a CSR graph, k and D).
+
+    The plan is built with ``external_workspace``: its per-call scratch (packed CBSR records,
+    selector words, the two-pass E x k products) is taken from torch's caching allocator on
+    the launch stream for every call, so no plan pins that memory and one plan can serve
+    several streams at once. The only mutation after creation, a value refresh, is ordered
+    after every earlier use on other streams (and every later use after it) with events.
+    """
 
     def __init__(self, ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k,
                  num_cols: Optional[int] = None, options: Optional[dict] = None):
@@ -138,6 +152,7 @@ class GraphPlan:
         self.dim_origin = int(dim_origin)
         self.dim_k = int(dim_k)
         opts = PlanOptions()
+        opts.external_workspace = 1
         for key, value in (options or {}).items():
             if key in ("fwd_accumulator", "bwd_accumulator") and isinstance(value, str):
                 value = ACC_KINDS[value]
@@ -147,6 +162,31 @@ class GraphPlan:
                                           self.num_cols, self.num_edges, self.dim_origin,
                                           self.dim_k, ctypes.byref(opts), _stream(),
                                           ctypes.byref(self.handle)), "maxk_plan_create")
+        fb, bb = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib.maxk_plan_workspace_bytes(self.handle, ctypes.byref(fb), ctypes.byref(bb)),
+              "maxk_plan_workspace_bytes")
+        self.external = bool(opts.external_workspace)
+        self.fwd_ws_bytes, self.bwd_ws_bytes = int(fb.value), int(bb.value)
+        self._uses = {}        # stream id -> (stream, event of its latest use)
+        self._refresh = None   # (stream, event) of the latest value refresh
+        self._lock = threading.Lock()
+
+    # -- stream ordering ------------------------------------------------------------------
+    def _begin(self, stream):
+        with self._lock:
+            if self._refresh is not None and self._refresh[0] != stream:
+                stream.wait_event(self._refresh[1])
+
+    def _end(self, stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        with self._lock:
+            self._uses[stream.cuda_stream] = (stream, ev)
+
+    def _workspace(self, nbytes):
+        if not self.external or nbytes == 0:
+            return None, 0
+        return torch.empty(nbytes, dtype=torch.uint8, device=self.device), nbytes
 
     def forward(self, sp_data, sp_index, out=None, accumulate: bool = False) -> torch.Tensor:
         """SpGEMM with this plan: sp tables [num_cols, k] -> out [num_rows, D];
@@ -157,10 +197,15 @@ class GraphPlan:
                 raise RuntimeError("accumulate=True needs an out tensor")
             out = torch.empty((self.num_rows, self.dim_origin), dtype=torch.float32,
                               device=sp_data.device)
-        fn = lib.maxk_spgemm_forward_acc if accumulate else lib.maxk_spgemm_forward
-        check(fn(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data), _p(sp_index), _p(out),
-                 self.num_rows, self.num_edges, self.dim_k, self.dim_origin, _stream()),
+        stream = torch.cuda.current_stream(self.device)
+        self._begin(stream)
+        ws, wsb = self._workspace(self.fwd_ws_bytes)
+        check(lib.maxk_spgemm_forward_ws(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
+                                         _p(sp_index), _p(out), self.num_rows, self.num_edges,
+                                         self.dim_k, self.dim_origin, int(accumulate), _p(ws),
+                                         wsb, ctypes.c_void_p(stream.cuda_stream)),
               "spgemm_forward")
+        self._end(stream)
         return out
 
     def backward(self, grad_out, sp_index, grad_sp=None) -> torch.Tensor:
@@ -169,23 +214,48 @@ class GraphPlan:
         if grad_sp is None:
             grad_sp = torch.empty((self.num_cols, self.dim_k), dtype=torch.float32,
                                   device=grad_out.device)
-        check(lib.maxk_sspmm_backward(self.handle, _p(ptr), _p(idx), _p(val), _p(grad_out),
-                                      _p(sp_index), _p(grad_sp), self.num_rows,
-                                      self.num_edges, self.dim_k, self.dim_origin, _stream()),
+        stream = torch.cuda.current_stream(self.device)
+        self._begin(stream)
+        ws, wsb = self._workspace(self.bwd_ws_bytes)
+        check(lib.maxk_sspmm_backward_ws(self.handle, _p(ptr), _p(idx), _p(val), _p(grad_out),
+                                         _p(sp_index), _p(grad_sp), self.num_rows,
+                                         self.num_edges, self.dim_k, self.dim_origin, _p(ws),
+                                         wsb, ctypes.c_void_p(stream.cuda_stream)),
               "spgemm_backward")
+        self._end(stream)
         return grad_sp
 
     def refresh_values(self, val: torch.Tensor) -> None:
+        """Re-snapshot in-place-modified edge values (same tensor, new ``_version``); runs
+        after every earlier use of the plan on any stream."""
+        stream = torch.cuda.current_stream(self.device)
+        with self._lock:
+            for other, ev in self._uses.values():
+                if other != stream:
+                    stream.wait_event(ev)
         with torch.cuda.device(self.device):
-            check(lib.maxk_plan_refresh_values(self.handle, _p(val), _stream()),
+            check(lib.maxk_plan_refresh_values(self.handle, _p(val),
+                                               ctypes.c_void_p(stream.cuda_stream)),
                   "maxk_plan_refresh_values")
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        with self._lock:
+            self._refresh = (stream, ev)
+            self._uses[stream.cuda_stream] = (stream, ev)
         self._refs = (self._refs[0], self._refs[1], val)
         self.val_version = val._version
 
     def info(self) -> dict:
         info = PlanInfo()
         check(lib.maxk_plan_get_info(self.handle, ctypes.byref(info)), "maxk_plan_get_info")
-        return info.as_dict()
+        d = info.as_dict()
+        d["fwd_workspace_bytes"] = self.fwd_ws_bytes
+        d["bwd_workspace_bytes"] = self.bwd_ws_bytes
+        return d
+
+    @property
+    def device_bytes(self) -> int:
+        return int(self.info()["device_bytes"])
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -194,30 +264,50 @@ class GraphPlan:
             self.handle = ctypes.c_void_p(0)
 
 
+# Plans are cached per (graph structure, edge-value tensor, k, D): two value sets on one
+# structure (SAGE 'mean' and GCN 'both' weights, say) get two plans instead of refreshing
+# one plan back and forth. The cache is bounded by the device memory the plans hold
+# (MAXK_PLAN_CACHE_BYTES, default a quarter of the device's HBM: ~72 GB on MI355X, twenty
+# Reddit-sized plans) and by a count.
 _PLAN_CACHE: "collections.OrderedDict[tuple, GraphPlan]" = collections.OrderedDict()
-_PLAN_CACHE_SIZE = 8
+_PLAN_CACHE_SIZE = 32
+_PLAN_CACHE_BYTES: Optional[int] = (int(os.environ["MAXK_PLAN_CACHE_BYTES"])
+                                    if "MAXK_PLAN_CACHE_BYTES" in os.environ else None)
 _PLAN_LOCK = threading.Lock()
 
 
+def _cache_budget(device) -> int:
+    if _PLAN_CACHE_BYTES is not None:
+        return _PLAN_CACHE_BYTES
+    return torch.cuda.get_device_properties(device).total_memory // 4
+
+
 def get_plan(ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k) -> GraphPlan:
-    """Cached plan for (graph storage, structure version, k, D); val changes are picked up
-    through ``val._version`` (in-place edits) or a new ``val`` tensor."""
+    """Cached plan for (graph storage, structure version, value tensor, k, D); in-place
+    edits of ``val`` (a new ``val._version``) refresh the plan's value snapshot."""
     key = (ptr.device.index, ptr.data_ptr(), idx.data_ptr(), ptr._version, idx._version,
-           int(num_nodes), int(num_edges), int(dim_origin), int(dim_k))
+           val.data_ptr(), int(num_nodes), int(num_edges), int(dim_origin), int(dim_k))
     with _PLAN_LOCK:
         plan = _PLAN_CACHE.get(key)
         if plan is not None:
             _PLAN_CACHE.move_to_end(key)
-            cached_val = plan._refs[2]
-            if cached_val is not val or plan.val_version != val._version:
+            if plan._refs[2] is not val or plan.val_version != val._version:
                 plan.refresh_values(val)
             return plan
         plan = GraphPlan(ptr, idx, val, int(num_nodes), int(num_edges), int(dim_origin),
                          int(dim_k))
         _PLAN_CACHE[key] = plan
-        while len(_PLAN_CACHE) > _PLAN_CACHE_SIZE:
-            _PLAN_CACHE.popitem(last=False)
+        budget = _cache_budget(ptr.device)
+        total = sum(p.device_bytes for p in _PLAN_CACHE.values())
+        while len(_PLAN_CACHE) > 1 and (len(_PLAN_CACHE) > _PLAN_CACHE_SIZE or total > budget):
+            _, old = _PLAN_CACHE.popitem(last=False)
+            total -= old.device_bytes
         return plan
+
+
+def cached_plan_bytes() -> int:
+    with _PLAN_LOCK:
+        return sum(p.device_bytes for p in _PLAN_CACHE.values())
 
 
 def clear_plan_cache() -> None:
@@ -255,11 +345,11 @@ def spgemm_forward(ptr, idx, val, sp_data, sp_index, num_nodes: int, num_edges: 
     _need(1 <= dim_k <= dim_origin <= 256, "k must be between 1 and input dimension")
     if plan is None:
         plan = get_plan(ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k)
-    out = torch.empty((num_nodes, dim_origin), dtype=torch.float32, device=sp_data.device)
+    _need(plan.num_rows == num_nodes and plan.num_edges == num_edges and
+          plan.dim_k == dim_k and plan.dim_origin == dim_origin,
+          "plan was built for a different graph / k / D")
     with torch.cuda.device(sp_data.device):
-        check(lib.maxk_spgemm_forward(plan.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
-                                      _p(sp_index), _p(out), num_nodes, num_edges, dim_k,
-                                      dim_origin, _stream()), "spgemm_forward")
+        out = plan.forward(sp_data, sp_index)
     return out, sp_index
 
 
@@ -280,11 +370,11 @@ def spgemm_backward(ptr, idx, val, grad_output, sp_index, num_nodes: int, num_ed
     _need(1 <= dim_k <= dim_origin <= 256, "k must be between 1 and input dimension")
     if plan is None:
         plan = get_plan(ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k)
-    grad_sp = torch.empty((num_nodes, dim_k), dtype=torch.float32, device=grad_output.device)
+    _need(plan.num_rows == num_nodes and plan.num_edges == num_edges and
+          plan.dim_k == dim_k and plan.dim_origin == dim_origin,
+          "plan was built for a different graph / k / D")
     with torch.cuda.device(grad_output.device):
-        check(lib.maxk_sspmm_backward(plan.handle, _p(ptr), _p(idx), _p(val), _p(grad_output),
-                                      _p(sp_index), _p(grad_sp), num_nodes, num_edges, dim_k,
-                                      dim_origin, _stream()), "spgemm_backward")
+        grad_sp = plan.backward(grad_output, sp_index)
     return grad_sp
 
 

@@ -53,13 +53,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, ret, phases=1):
+def _worker(rank, world, port, ret, phases=1, size=(700, 15_000)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from oracle import oracle
-        n, d, k = 700, 32, 8
-        ptr, idx = graphs.synthetic_csr(n, 15_000, seed=3)
+        (n, e), d, k = size, 32, 8
+        ptr, idx = graphs.synthetic_csr(n, e, seed=3)
         val = graphs.sage_mean_values(ptr)
         x = graphs.features(n, d, seed=1)
         g = graphs.features(n, d, seed=2)
@@ -101,14 +101,16 @@ def _worker(rank, world, port, ret, phases=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,phases", [(2, 1), (2, 2), (3, 2)])
-def test_sharded_aggregation_matches_single(world, phases):
+@pytest.mark.parametrize("world,phases,size", [(2, 1, (700, 15_000)), (2, 2, (700, 15_000)),
+                                               (3, 2, (700, 15_000)),
+                                               (4, 1, (20_000, 600_000))])
+def test_sharded_aggregation_matches_single(world, phases, size):
     from oracle import oracle
     mgr = mp.Manager()
     ret = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), ret, phases), nprocs=world, join=True)
-    n, d, k = 700, 32, 8
-    ptr, idx = graphs.synthetic_csr(n, 15_000, seed=3)
+    mp.spawn(_worker, args=(world, _free_port(), ret, phases, size), nprocs=world, join=True)
+    (n, e), d, k = size, 32, 8
+    ptr, idx = graphs.synthetic_csr(n, e, seed=3)
     val = graphs.sage_mean_values(ptr)
     x = graphs.features(n, d, seed=1).numpy()
     g = graphs.features(n, d, seed=2).numpy()

@@ -1,0 +1,180 @@
+"""GPU, the two BASELINE.json configs that have no kernel of their own in the bench:
+
+* config 1 — "flickr GraphSAGE hidden=64 ReLU baseline on DGL CPU SpMM path": the ReLU
+  layers' dense aggregation (maxk_kernels.dense_aggregate: HIP CSR SpMM forward, the same
+  kernel on the transposed CSR backward) on the Flickr-shaped graph (N=89,250,
+  E=989,006 + self-loops, synthetic), hidden 64, checked against the oracle's DGL
+  update_all(copy_u, mean) restatement, plus a MaxKSAGE(nonlinear='relu') training step;
+* config 5 — "Reddit row-partitioned across 8 x MI355X": the full-size W=8 RowPartition with
+  every rank's rectangular plans run on this one GPU and the all-gather / reduce-scatter
+  emulated with tensor ops (the real collectives are covered by tests/test_dist.py over
+  gloo and test_gpu_dist.py over RCCL), checked by the adjoint identity, linearity against
+  the single-GPU plan and oracle-sampled rows and columns.
+"""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import maxk_kernels as mk
+from maxk_kernels import graphs
+from maxk_kernels.dist import RowPartition
+from oracle import oracle
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+
+def _transpose(ptr, idx, val):
+    n = ptr.size - 1
+    rows = np.repeat(np.arange(n, dtype=np.int32), np.diff(ptr))
+    order = np.argsort(idx, kind="stable")
+    pt = np.zeros(n + 1, np.int32)
+    pt[1:] = np.cumsum(np.bincount(idx, minlength=n))
+    return pt, rows[order], val[order]
+
+
+def test_config1_flickr_relu_dense_aggregation(gpu):
+    n, e = graphs.DATASETS["flickr"]
+    ptr, idx = graphs.synthetic_csr(n, e, seed=97)
+    p, ix = ptr.numpy(), idx.numpy()
+    csr = mk.CSRGraph(ptr.to(gpu), idx.to(gpu)).with_values("mean")
+    x = torch.relu(graphs.features(n, 64, seed=97))          # ReLU input, hidden 64
+    g = graphs.features(n, 64, seed=98)
+    xg = x.to(gpu).requires_grad_(True)
+    y = mk.dense_aggregate(xg, csr)
+    y.backward(g.to(gpu))
+    torch.cuda.synchronize()
+    # DGL update_all(copy_u, mean) (oracle, f32) and the per-element sum of |terms|
+    ref = oracle.dense_spmm(p, ix, None, x.numpy(), mean=True)
+    w = csr.val.cpu().numpy()
+    mag = oracle.dense_spmm(p, ix, w, np.abs(x.numpy()))
+    ok, worst = oracle.close_enough(y.detach().cpu().numpy(), ref, mag)
+    assert ok, worst
+    pt, it, wt = _transpose(p, ix, w)
+    ref_b = oracle.dense_spmm(pt, it, wt, g.numpy())
+    mag_b = oracle.dense_spmm(pt, it, wt, np.abs(g.numpy()))
+    ok, worst = oracle.close_enough(xg.grad.cpu().numpy(), ref_b, mag_b)
+    assert ok, worst
+    # timing of the config-1 aggregation on the GPU (printed; the CPU figure is bench.py's
+    # cpu_baseline / tools/cpu_config1.py)
+    xd = x.to(gpu)
+    for _ in range(3):
+        mk.dense_aggregate(xd, csr)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        mk.dense_aggregate(xd, csr)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / 20 * 1e3
+    print(f"flickr hidden 64 dense aggregation (mean): {ms:.3f} ms, {e / ms / 1e6:.2f} G edges/s")
+
+
+def test_config1_flickr_relu_sage_trains(gpu):
+    """MaxKSAGE(nonlinear='relu') built as maxk_gnn_integrated.py:317-321 builds it, on the
+    Flickr-shaped graph with Flickr's 500 input features and 7 classes: a few steps run and
+    fit the (random) labels."""
+    n, e = graphs.DATASETS["flickr"]
+    ptr, idx = graphs.synthetic_csr(n, e, seed=97, device=gpu)
+    csr = mk.CSRGraph(ptr, idx)
+    torch.manual_seed(0)
+    feats = graphs.features(n, 500, seed=3, device=gpu)
+    labels = torch.randint(0, 7, (n,), device=gpu)
+    model = mk.MaxKSAGE(500, 64, 3, 7, 32, feat_drop=0.2, norm=True, nonlinear="relu").to(gpu)
+    opt = torch.optim.Adam(model.parameters(), lr=0.01)
+    losses = []
+    for _ in range(15):
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(model(csr, feats), labels)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert np.isfinite(losses).all() and losses[-1] < losses[0]
+
+
+def _sampled_rows_ok(y, ptr, idx, val, sp_data, sp_index, D, nrows=1500, seed=0):
+    N = ptr.numel() - 1
+    p = ptr.cpu().numpy()
+    deg = np.diff(p)
+    rows = np.unique(np.concatenate([np.random.RandomState(seed).choice(N, nrows, replace=False),
+                                     np.argsort(deg)[-8:]]))
+    ix, v = idx.cpu().numpy(), val.cpu().numpy()
+    sub_ptr = np.zeros(N + 1, np.int32)
+    sub_ptr[1:rows.size + 1] = np.cumsum(deg[rows])
+    sub_ptr[rows.size + 1:] = sub_ptr[rows.size]
+    sub_idx = np.concatenate([ix[p[r]:p[r + 1]] for r in rows])
+    sub_val = np.concatenate([v[p[r]:p[r + 1]] for r in rows])
+    ref, mag = oracle.spgemm_forward(sub_ptr, sub_idx, sub_val, sp_data.cpu().numpy(),
+                                     sp_index.cpu().numpy(), D, with_mag=True)
+    got = y[torch.from_numpy(rows).to(y.device)].cpu().numpy()
+    return oracle.close_enough(got, ref[:rows.size], mag[:rows.size])
+
+
+def _sampled_cols_ok(gs, ptr, idx, val, sp_index, g, ncols=400, seed=1):
+    N, K = sp_index.shape
+    cols = np.random.RandomState(seed).choice(N, ncols, replace=False)
+    ix = idx.cpu().numpy()
+    e_ids = np.nonzero(np.isin(ix, cols))[0]
+    rows_of = np.repeat(np.arange(N), np.diff(ptr.cpu().numpy()))[e_ids]
+    c = ix[e_ids]
+    v = val.cpu().numpy()[e_ids].astype(np.float64)
+    si = sp_index.cpu().numpy()
+    terms = v[:, None] * g.cpu().numpy()[rows_of[:, None], si[c].astype(np.int64)]
+    ref = np.zeros((N, K))
+    mag = np.zeros((N, K))
+    np.add.at(ref, c, terms)
+    np.add.at(mag, c, np.abs(terms))
+    return oracle.close_enough(gs.cpu().numpy()[cols], ref[cols], mag[cols])
+
+
+@pytest.mark.parametrize("k", [16])
+def test_config5_reddit_w8_partition(gpu, k):
+    D, W = 256, 8
+    n, e = graphs.DATASETS["reddit"]
+    ptr, idx = graphs.synthetic_csr(n, e, seed=97, device=gpu)
+    val = graphs.sage_mean_values(ptr)
+    h = graphs.features(n, D, seed=97, device=gpu)
+    g = graphs.features(n, D, seed=98, device=gpu)
+    sp_data, sp_index = mk.maxk_forward(h, k, return_index=True)
+    del h
+    part = RowPartition(ptr, W)
+    assert part.phases == 1 and part.padded_rows >= n
+    # the padded all-gather tables every rank holds after the forward exchange
+    table_d = torch.zeros((part.padded_rows, k), device=gpu)
+    table_i = torch.zeros((part.padded_rows, k), dtype=torch.uint8, device=gpu)
+    for q in range(W):
+        a, b = part.rows(q)
+        pos = part.table_positions(q, gpu)
+        table_d[pos] = sp_data[a:b]
+        table_i[pos] = sp_index[a:b]
+    y = torch.empty((n, D), device=gpu)
+    grad_table = torch.zeros((part.padded_rows, k), device=gpu)
+    ranks_e = []
+    for q in range(W):
+        a, b = part.rows(q)
+        lp, li, lv = part.local_csr(ptr, idx, val, q)
+        ranks_e.append(li.numel())
+        plan = mk.GraphPlan(lp, li, lv, b - a, li.numel(), D, k, num_cols=part.phase_cols)
+        y[a:b] = plan.forward(table_d, table_i)
+        grad_table += plan.backward(g[a:b].contiguous(), table_i)     # the reduce-scatter
+        del plan
+    torch.cuda.synchronize()
+    gs = torch.cat([grad_table[part.table_positions(q, gpu)] for q in range(W)])
+    # nnz balance of the partition: every rank within 1 % of E / W
+    assert max(ranks_e) <= 1.01 * e / W and sum(ranks_e) == e
+    # adjoint identity <A densify(sp), G> = <sp, SSpMM(G)>
+    lhs = (y.double() * g.double()).sum().item()
+    rhs = (sp_data.double() * gs.double()).sum().item()
+    scale = (y.double().abs() * g.double().abs()).sum().item()
+    assert abs(lhs - rhs) <= 1e-5 * scale
+    # the single-GPU plan on the whole graph gives the same sums
+    y1, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, n, e, k, D)
+    g1 = mk.spgemm_backward(ptr, idx, val, g, sp_index, n, e, k, D)
+    assert ((y - y1).abs() <= 2e-5 * y1.abs().max()).all()
+    assert ((gs - g1).abs() <= 2e-5 * g1.abs().max()).all()
+    del y1, g1
+    mk.clear_plan_cache()
+    ok, worst = _sampled_rows_ok(y, ptr, idx, val, sp_data, sp_index, D)
+    assert ok, worst
+    ok, worst = _sampled_cols_ok(gs, ptr, idx, val, sp_index, g)
+    assert ok, worst

@@ -458,3 +458,119 @@ def test_rocsparse_comparator_vs_oracle(gpu):
     y, ms = baselines.spmm_rocsparse(ptr, idx, val, x.to(gpu), times=2)
     assert ms > 0
     assert_close(y, ref, mag, rtol=2e-6 * 64)
+
+
+# ------------------------------------------------------------------------ streams / scratch
+def test_two_streams_share_one_plan(gpu):
+    """One cached plan used from two streams at once: each call takes its scratch (packed
+    records, selector words) from the caching allocator on its own stream, so concurrent
+    forward/backward calls on different inputs all match the oracle."""
+    ptr, idx = graphs.synthetic_csr(20_000, 3_000_000, seed=31)
+    val = graphs.sage_mean_values(ptr)
+    n, d, k = 20_000, 256, 16
+    dptr, didx, dval = ptr.to(gpu), idx.to(gpu), val.to(gpu)
+    plan = mk.get_plan(dptr, didx, dval, n, idx.numel(), d, k)
+    assert plan.fwd_ws_bytes > 0 and plan.bwd_ws_bytes > 0
+    xs = [graphs.features(n, d, seed=40 + j) for j in range(2)]
+    gs = [graphs.features(n, d, seed=50 + j) for j in range(2)]
+    sps = [oracle.maxk(x.numpy(), k) for x in xs]
+    streams = [torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)]
+    torch.cuda.synchronize()
+    outs = [[], []]
+    for rep in range(3):
+        for j, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                sd, si = to_dev(sps[j][0], gpu), to_dev(sps[j][1], gpu)
+                y, _ = mk.spgemm_forward(dptr, didx, dval, sd, si, n, idx.numel(), k, d)
+                g = mk.spgemm_backward(dptr, didx, dval, to_dev(gs[j].numpy(), gpu), si, n,
+                                       idx.numel(), k, d)
+                outs[j].append((y, g))
+    torch.cuda.synchronize()
+    for j in range(2):
+        ref, mag = oracle.spgemm_forward(ptr.numpy(), idx.numpy(), val.numpy(), *sps[j], d,
+                                         with_mag=True)
+        gref, gmag = oracle.sspmm_backward(ptr.numpy(), idx.numpy(), val.numpy(),
+                                           gs[j].numpy(), sps[j][1], with_mag=True)
+        for y, g in outs[j]:
+            assert_close(y, ref, mag)
+            assert_close(g, gref, gmag)
+
+
+def test_value_refresh_is_ordered_after_other_streams(gpu):
+    """In-place edge-value edits re-snapshot the cached plan on the editing stream only
+    after the plan's earlier uses on other streams: a forward queued on stream A keeps the
+    old values, the one on stream B after the edit sees the new ones."""
+    ptr, idx = graphs.synthetic_csr(30_000, 3_000_000, seed=33)
+    val = graphs.sage_mean_values(ptr)
+    n, d, k = 30_000, 256, 16
+    dptr, didx, dval = ptr.to(gpu), idx.to(gpu), val.to(gpu)
+    od, oi = oracle.maxk(graphs.features(n, d, seed=60).numpy(), k)
+    sd, si = to_dev(od, gpu), to_dev(oi, gpu)
+    mk.spgemm_forward(dptr, didx, dval, sd, si, n, idx.numel(), k, d)   # build the plan
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    with torch.cuda.stream(a):
+        ys = [mk.spgemm_forward(dptr, didx, dval, sd, si, n, idx.numel(), k, d)[0]
+              for _ in range(6)]                                          # a long queue on A
+    with torch.cuda.stream(b):
+        dval.mul_(2.0)
+        y2, _ = mk.spgemm_forward(dptr, didx, dval, sd, si, n, idx.numel(), k, d)
+    torch.cuda.synchronize()
+    ref, mag = oracle.spgemm_forward(ptr.numpy(), idx.numpy(), val.numpy(), od, oi, d,
+                                     with_mag=True)
+    for y in ys:
+        assert_close(y, ref, mag)
+    assert_close(y2, 2 * ref, 2 * mag)
+
+
+def test_capi_external_workspace_contract(gpu):
+    """A plan created with external_workspace holds no scratch: the plain entry points
+    refuse it, the *_ws ones take a caller buffer of maxk_plan_workspace_bytes (and refuse
+    a smaller one)."""
+    import ctypes
+    from maxk_kernels import _lib
+    ptr, idx = graphs.synthetic_csr(5000, 200_000, seed=35)
+    val = graphs.sage_mean_values(ptr)
+    n, d, k = 5000, 256, 16
+    dptr, didx, dval = ptr.to(gpu), idx.to(gpu), val.to(gpu)
+    od, oi = oracle.maxk(graphs.features(n, d, seed=61).numpy(), k)
+    sd, si = to_dev(od, gpu), to_dev(oi, gpu)
+    plan = mk.GraphPlan(dptr, didx, dval, n, idx.numel(), d, k, options={"fwd_two_tables": 2})
+    assert plan.fwd_ws_bytes == n * 128            # one 128-B packed record per node
+    out = torch.empty((n, d), device=gpu)
+    P = ctypes.c_void_p
+    s = P(torch.cuda.current_stream().cuda_stream)
+    args = (plan.handle, P(dptr.data_ptr()), P(didx.data_ptr()), P(dval.data_ptr()),
+            P(sd.data_ptr()), P(si.data_ptr()), P(out.data_ptr()), n, idx.numel(), k, d)
+    assert _lib.lib.maxk_spgemm_forward(*args, s) == -1
+    small = torch.empty(plan.fwd_ws_bytes - 16, dtype=torch.uint8, device=gpu)
+    assert _lib.lib.maxk_spgemm_forward_ws(*args, 0, P(small.data_ptr()), small.numel(), s) == -1
+    ws = torch.empty(plan.fwd_ws_bytes, dtype=torch.uint8, device=gpu)
+    assert _lib.lib.maxk_spgemm_forward_ws(*args, 0, P(ws.data_ptr()), ws.numel(), s) == 0
+    torch.cuda.synchronize()
+    ref, mag = oracle.spgemm_forward(ptr.numpy(), idx.numpy(), val.numpy(), od, oi, d,
+                                     with_mag=True)
+    assert_close(out, ref, mag)
+
+
+def test_ref_compat_padding_slots_carry_no_gradient(gpu):
+    """Rows where the reference bisection fills fewer than k slots: the (0.0f, 0) padding
+    slots must not write a gradient into feature 0 unless feature 0 was selected."""
+    k, d = 16, 256
+    rs = np.random.RandomState(7)
+    x = rs.rand(64, d).astype(np.float32)
+    x[::2, 123] = 1e6          # even rows: one hit, 15 padding slots; feature 0 not selected
+    x[1::4, 0] = 5e6           # rows 1, 5, ...: feature 0 is the single hit
+    xt = to_dev(x, gpu).requires_grad_(True)
+    sp_data, sp_index = mk.maxk(xt, k, mode="ref_compat")
+    w = torch.randn(64, k, device=gpu)
+    (sp_data * w).sum().backward()
+    od, oi = oracle.maxk(x, k, "ref_compat")
+    assert np.array_equal(sp_index.cpu().numpy(), oi)
+    expect = np.zeros_like(x)
+    wn = w.cpu().numpy()
+    for r in range(64):
+        for j in range(k):
+            if od[r, j] != 0 or (j == 0 and x[r, oi[r, 0]] > 0):   # a filled slot
+                expect[r, oi[r, j]] = wn[r, j]
+    assert np.array_equal(xt.grad.cpu().numpy(), expect)
