@@ -31,6 +31,9 @@ import maxk_kernels as mk  # noqa: E402
 from maxk_kernels import graphs  # noqa: E402
 from maxk_kernels.dist import RowPartition, ShardedAggregation  # noqa: E402
 
+# BASELINE.json "metric", verbatim: the primary line is k=16 (config.workload), the other k
+# of the set are the k_sweep entries
+METRIC = "SpGEMM+SSpMM edges/sec on Reddit, hidden=256, k in {8,16,32,64}; %HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # L1-miss line-request ceiling: ~1 request of 128 B per ns per CU for L2-resident gathers
 # (tools/ubench_tcp.hip, profiles/r01/ubench_tcp.log), x 256 CUs
@@ -135,6 +138,9 @@ def cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d, sample_frac, reps, log_
         "cores": oracle.num_threads(),
         "cpu_model": cpu_model(),
         "host_cpus": os.cpu_count(),
+        "affinity_cpus": len(os.sched_getaffinity(0)),
+        "cores_note": ("OpenMP threads = the lease's CPU share (OMP_NUM_THREADS, set by the GPU "
+                       "pool per GPU; host_cpus / affinity_cpus count the whole machine)"),
         "kind": "port",
         "sample": (f"DGL-semantics dense CSR SpMM (oracle C/OpenMP, f32): forward A@X over "
                    f"rows [0,{r_f}) = {e_f} edges and backward A^T@G over rows [0,{r_b}) of "
@@ -285,7 +291,7 @@ def main():
             traffic = None
 
     result = {
-        "metric": "SpGEMM+SSpMM edges/sec on Reddit, hidden=256, k=16; %HBM roofline",
+        "metric": METRIC,
         "value": value,
         "unit": "edges/s",
         "n_gpus": world,
@@ -340,12 +346,31 @@ def main():
         "cpu_baseline": None,
     }
 
+    def sweep_traffic(ks, tf, tb):
+        """PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE per launch, profiles/pmc_traffic.json) of
+        the k's forward and backward kernels, its rate, and its ratio to the algorithmic
+        bytes (traffic well above the compulsory bytes = re-reads)."""
+        ent = {}
+        try:
+            ent = json.load(open(args.traffic_json)).get(f"{args.dataset}:k{ks}:d{d}:n1", {})
+        except (OSError, ValueError):
+            pass
+        out = {}
+        for dirn, kern, t, ab in (("fwd", "spgemm_fwd", tf, fwd_bytes(n, e, ks, d)),
+                                  ("bwd", "sspmm_bwd", tb, bwd_bytes(n, e, ks, d))):
+            tr = ent.get(kern)
+            out[f"{dirn}_traffic"] = tr
+            out[f"{dirn}_traffic_ratio"] = None if tr is None else tr / ab
+            out[f"{dirn}_traffic_GBps"] = None if tr is None else tr / (t * 1e-3) / 1e9
+        return out
+
     if world == 1 and args.k_sweep:
         # the metric's k in {8,16,32,64}: same graph and features, kernel device time only
         sweep = {str(k): {"fwd_ms": fwd_ms, "bwd_ms": bwd_ms,
                           "edges_per_s": 2 * e / ((fwd_ms + bwd_ms) * 1e-3),
                           "fwd_roofline_frac": fwd_gbs / HBM_PEAK_GBS,
                           "bwd_roofline_frac": bwd_gbs / HBM_PEAK_GBS}}
+        sweep[str(k)].update(sweep_traffic(k, fwd_ms, bwd_ms))
         h_full = graphs.features(n, d, seed=97, device=dev)
         for ks in [int(x) for x in args.k_sweep.replace('"', "").split(",") if x.strip()]:
             if ks == k:
@@ -364,6 +389,7 @@ def main():
                 "fwd_roofline_frac": fwd_bytes(n, e, ks, d) / (tf * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "bwd_roofline_frac": bwd_bytes(n, e, ks, d) / (tb * 1e-3) / 1e9 / HBM_PEAK_GBS,
             }
+            sweep[str(ks)].update(sweep_traffic(ks, tf, tb))
             log(f"k={ks}: fwd {tf:.3f} ms bwd {tb:.3f} ms")
             del p, sd, si, o, gr
         del h_full

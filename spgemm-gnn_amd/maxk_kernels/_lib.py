@@ -87,6 +87,8 @@ class PlanOptions(ctypes.Structure):
         ("fwd_rot_windows", _i32),
         ("fwd_rot_rate", _i32),
         ("external_workspace", _i32),
+        ("fwd_sync", _i32),
+        ("fwd_sync_lag", _i32),
     ]
 
 

@@ -1,5 +1,6 @@
-"""Small fixed workload for rocprofv3 --pmc passes (tooling): the BASELINE config (Reddit,
-D=256, k=16), 3 SpGEMM forwards + 3 SSpMM backwards with the default plan."""
+"""Small fixed workload for rocprofv3 --pmc passes (tooling): one dataset-shaped synthetic
+graph (PMC_DATASET, default reddit), D=256, k=PMC_K, SAGE-mean or GCN values (PMC_KIND),
+1 + 3 SpGEMM forwards and 1 + 3 SSpMM backwards with the default (or PMC_OPTS) plan."""
 import json
 import os
 import sys
@@ -13,17 +14,18 @@ from maxk_kernels import graphs  # noqa: E402
 
 k = int(os.environ.get("PMC_K", "16"))
 ds = os.environ.get("PMC_DATASET", "reddit")
+kind = os.environ.get("PMC_KIND", "sage")
 dev = torch.device("cuda:0")
 n, e = graphs.DATASETS[ds]
 ptr, idx = graphs.synthetic_csr(n, e, device=dev)
-val = graphs.sage_mean_values(ptr)
+val = graphs.sage_mean_values(ptr) if kind == "sage" else graphs.gcn_values(ptr, idx)
 e = idx.numel()
 h = graphs.features(n, 256, seed=97, device=dev)
 g = graphs.features(n, 256, seed=98, device=dev)
 sp_data, sp_index = mk.maxk_forward(h, k, return_index=True)
+del h
 opts = json.loads(os.environ.get("PMC_OPTS", "{}"))
-plan = mk.GraphPlan(ptr, idx, val, n, e, 256, k, options=opts) if opts else mk.get_plan(
-    ptr, idx, val, n, e, 256, k)
+plan = mk.GraphPlan(ptr, idx, val, n, e, 256, k, options=opts)
 out = plan.forward(sp_data, sp_index)
 grad = plan.backward(g, sp_index)
 for _ in range(3):
