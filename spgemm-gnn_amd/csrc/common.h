@@ -35,8 +35,6 @@ constexpr int kBwdTasksPerCu = 2;
 constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k atomics) vs its edges
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
-constexpr int kFwdSyncWindows = 32;        // column windows of the paced (fwd_sync) sweep
-constexpr int kFwdSyncBytes = 8 * 128;     // pacing counters: one 128-B line per XCD label
 constexpr double kFwdSlotEdgeRate = 1.6e8;  // edges/s one forward slot sustains at k = 16
 // CBSR tables (5k bytes per column) above these sizes get packed one-line forward records
 // even where two tables would otherwise be used (plan.hip: k >= 32 / k < 32)
@@ -155,8 +153,6 @@ struct maxk_plan {
   int32_t fwd_phases = 1;        // column phases per forward call
   int32_t fwd_persistent = 0;    // grid = resident capacity (1) or one work-group per task
   int32_t fwd_rot_ticks = 0;     // > 0: rotated sweeps, s_memrealtime ticks per window
-  int32_t fwd_sync = 0;          // paced window sweep on a persistent grid (counters in ws)
-  int32_t fwd_sync_lag = 1;      // windows a work-group may run ahead of its label's average
   int32_t fwd_unroll = 8;        // independent sub-steps per wave (8 or 16)
   int32_t bwd_unroll = 8;
   int32_t fwd_waves = 4;         // wavefronts per forward work-group

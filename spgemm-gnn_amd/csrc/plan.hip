@@ -344,8 +344,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.external_workspace == 0 || o.external_workspace == 1,
                  "maxk_plan_create: external_workspace must be 0 or 1");
-  MAXK_CHECK_ARG(o.fwd_sync >= 0 && o.fwd_sync <= 2 && o.fwd_sync_lag >= 0 && o.fwd_sync_lag <= 64,
-                 "maxk_plan_create: fwd_sync must be 0, 1 or 2 and fwd_sync_lag in [0, 64]");
   maxk_plan* p = new maxk_plan();
   p->external_ws = o.external_workspace;
   p->num_nodes = N;
@@ -509,13 +507,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     int B = o.fwd_phases;
     p->fwd_persistent = o.fwd_persistent ? 1 : 0;
     p->fwd_rot_ticks = 0;
-    // paced window sweep (fwd_sync): a persistent grid whose work-groups walk the same
-    // column windows per XCD (spgemm_fwd_kernel); the 4-features-per-lane paths only
-    p->fwd_sync = o.fwd_sync == 1 && B <= 1 && (k % 4 == 0 || p->fwd_chunk3) && nt > 0;
-    p->fwd_sync_lag = o.fwd_sync_lag > 0 ? o.fwd_sync_lag : 1;
-    if (p->fwd_sync) {
-      B = o.fwd_rot_windows > 0 ? std::min(o.fwd_rot_windows, 64) : kFwdSyncWindows;
-    } else if (B <= 1 && o.fwd_rotate != 2 && (k % 4 == 0 || p->fwd_chunk3) && nt > 0) {
+    if (B <= 1 && o.fwd_rotate != 2 && (k % 4 == 0 || p->fwd_chunk3) && nt > 0) {
       B = o.fwd_rot_windows > 0 ? std::min(o.fwd_rot_windows, 64) : kFwdRotWindows;
       // one turn of the clock per tile: the measured per-slot rate scales as ~1/k (Reddit:
       // 2.4e8, 1.65e8, 0.9e8 edges/s per slot at k = 8, 16, 32; best sweep rates 300, 150-200,
@@ -572,7 +564,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes : cbsr_record_bytes(k);
     p->fwd_ws_bytes = (int64_t)NC * p->fwd_rec_bytes;
   }
-  if (p->fwd_sync) p->fwd_ws_bytes += kFwdSyncBytes;  // pacing counters ahead of the records
   if (p->fwd_ws_bytes > 0 && !p->external_ws) {  // plan-owned per-call pack buffer
     PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)p->fwd_ws_bytes));
     p->device_bytes += p->fwd_ws_bytes;

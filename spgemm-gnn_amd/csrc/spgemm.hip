@@ -229,25 +229,11 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     int phases, int phase, const uint2* __restrict__ cv,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
     const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
-    int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab, int accum,
-    uint32_t* __restrict__ sync_ctr, int sync_lag, int sync_max_tasks) {
+    int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab, int accum) {
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
   T* acc = reinterpret_cast<T*>(smem_d);
-  // Soft-synchronised sweep (sync_ctr != nullptr, persistent grid): the work-groups that
-  // share an XCD (blockIdx % 8, a label used for speed only) walk the column windows of
-  // their tasks in step, so the window of the CBSR table they gather from stays in that
-  // XCD's L2. Each work-group adds 1 to its label's counter per finished window; before a
-  // window it waits (bounded spin) until the label's average progress is within sync_lag
-  // windows of its own. The counter only paces; no result depends on it, a wait that times
-  // out switches the pacing off for the work-group, and an exiting work-group adds the
-  // progress it will never make so the others are not held back.
-  const int label = blockIdx.x & (kXcds - 1);
-  const int members = (int)((gridDim.x - label + kXcds - 1) / kXcds);
-  uint32_t* ctr = sync_ctr ? sync_ctr + label * 32 : nullptr;  // one 128-B line per label
-  int progress = 0;
-  bool pace = true;  // thread 0 only
   // Work-group w runs tasks w, w + G, ... (G = grid size; G = #tasks by default, or the
   // resident capacity with the fwd_persistent option, which measured slower on Reddit).
   // rot_ticks > 0: one launch, each task's sweep rotated to start at the window of the
@@ -256,10 +242,7 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   FwdTask t = tasks[ti];
   int emid = -1;
   __shared__ int s_w0;
-  if (ctr) {
-    t.e0 = phase_off[ti * (phases + 1)];
-    t.e1 = phase_off[ti * (phases + 1) + phases];
-  } else if (rot_ticks > 0) {
+  if (rot_ticks > 0) {
     // start the column-sorted sweep at the window the clock points to, wrapping around
     // (read once per work-group: every wave must split the task at the same edge)
     __syncthreads();
@@ -274,7 +257,7 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   t.e0 = phase_off[ti * (phases + 1) + phase];
   t.e1 = phase_off[ti * (phases + 1) + phase + 1];
   }
-  if (!ctr && (phase > 0 || accum) && t.e0 == t.e1) continue;  // nothing to add (uniform)
+  if ((phase > 0 || accum) && t.e0 == t.e1) continue;  // nothing to add (uniform)
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
   const int n = nrows * D;
@@ -308,34 +291,7 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     // chain (col, val) -> CBSR record -> LDS has two dependent global round trips, so
     // memory-level parallelism comes from U independent sub-steps per wave. Out-of-range
     // lanes load a clamped (valid) edge and skip the update.
-    if (ctr) {
-      // the task's column windows in order; each wave takes a contiguous share of a window
-      const int32_t* off = phase_off + (size_t)ti * (phases + 1);
-      for (int w = 0; w < phases; ++w) {
-        if (threadIdx.x == 0 && pace) {
-          const uint32_t need = (uint32_t)max(0, progress - sync_lag) * (uint32_t)members;
-          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-            __builtin_amdgcn_s_sleep(2);
-            // 100 us (100 MHz clock): a member that is not resident, or far behind; stop
-            // pacing this work-group for the rest of the launch
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 10000) {
-              pace = false;
-              break;
-            }
-          }
-        }
-        __syncthreads();
-        const int a = off[w], b = off[w + 1];
-        const int len = b - a;
-        fwd_edges4<U, A, FL>(acc, a + (int)((int64_t)len * wave / kWaves),
-                             a + (int)((int64_t)len * (wave + 1) / kWaves), 0, 1, EPS, slot,
-                             l0, lane_on, cv, rec, rec_bytes, seltab, DS, k);
-        ++progress;
-        if (threadIdx.x == 0)
-          __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else if (emid >= 0) {
+    if (emid >= 0) {
       fwd_edges4<U, A, FL>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, seltab, DS, k);
       fwd_edges4<U, A, FL>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
@@ -375,12 +331,6 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     for (int i = threadIdx.x; i < D; i += NT) global_add(dst + i, get(i));
   }
   }  // task loop
-  if (ctr && threadIdx.x == 0) {  // the windows this work-group will not run
-    const int total = sync_max_tasks * phases;
-    if (total > progress)
-      __hip_atomic_fetch_add(ctr, (uint32_t)(total - progress), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, float* out,
@@ -1153,8 +1103,7 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   MAXK_CHECK_ARG(out && sp_data && sp_index && (E == 0 || (idx && val)) && ptr,
                  "maxk_spgemm_forward: null pointer");
   (void)val;  // the plan holds the permuted snapshot of (idx, val)
-  // workspace: [pacing counters, kFwdSyncBytes, with fwd_sync][packed CBSR records]
-  uint8_t* ws_base = plan->fwd_rec;
+  uint8_t* ws_base = plan->fwd_rec;  // packed CBSR records (per call)
   if (ws) {
     MAXK_CHECK_ARG(ws_bytes >= plan->fwd_ws_bytes,
                    "maxk_spgemm_forward: workspace smaller than maxk_plan_workspace_bytes");
@@ -1164,13 +1113,7 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     return MAXK_ERR_INVALID_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  uint32_t* sync_ctr = nullptr;
   uint8_t* rec_ws = ws_base;
-  if (plan->fwd_sync) {
-    sync_ctr = reinterpret_cast<uint32_t*>(ws_base);
-    rec_ws = ws_base + kFwdSyncBytes;
-    MAXK_HIP_TRY(hipMemsetAsync(sync_ctr, 0, kFwdSyncBytes, s));
-  }
   if (plan->n_zero_rows > 0 && !accum) {  // split rows are summed atomically into zeroed rows
     hipLaunchKernelGGL(zero_rows_kernel, dim3(plan->n_zero_rows), dim3(256), 0, s,
                        plan->zero_rows, plan->n_zero_rows, out, D);
@@ -1208,16 +1151,14 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     int per_cu = 0;                                                                       \
     MAXK_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(                            \
         &per_cu, spgemm_fwd_kernel<V, A, UU, NT, FL>, NT, lds));                          \
-    const int g = (plan->fwd_persistent || sync_ctr)                                      \
+    const int g = plan->fwd_persistent                                                    \
                       ? std::max(1, std::min(plan->n_fwd_tasks, std::max(per_cu, 1) * plan->cus)) \
                       : plan->n_fwd_tasks;                                                \
-    const int max_tasks = (plan->n_fwd_tasks + g - 1) / g;                                \
-    for (int b = 0; b < ((rot || sync_ctr) ? 1 : B); ++b)                                 \
+    for (int b = 0; b < (rot ? 1 : B); ++b)                                               \
       hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU, NT, FL>), dim3(g), dim3(NT), lds, s, \
                          plan->fwd_tasks, plan->n_fwd_tasks, plan->fwd_phase_off, B, b,   \
                          plan->fwd_cv, sp_data, sp_index, recp,                           \
-                         rec_bytes_eff, out, D, k, R, rot, seltab, accum,                 \
-                         (V == 4) ? sync_ctr : nullptr, plan->fwd_sync_lag, max_tasks);   \
+                         rec_bytes_eff, out, D, k, R, rot, seltab, accum);                \
   } while (0)
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \

@@ -87,8 +87,6 @@ class PlanOptions(ctypes.Structure):
         ("fwd_rot_windows", _i32),
         ("fwd_rot_rate", _i32),
         ("external_workspace", _i32),
-        ("fwd_sync", _i32),
-        ("fwd_sync_lag", _i32),
     ]
 
 

@@ -383,9 +383,6 @@ PLAN_OPTIONS = [
     dict(fwd_accumulator="f32_cas"), dict(fwd_tile_rows=64, fwd_accumulator="f32_cas"),
     dict(fwd_phases=3), dict(fwd_persistent=1), dict(fwd_unroll=16), dict(fwd_task_cap=512),
     dict(fwd_rotate=2), dict(fwd_persistent=1, fwd_rotate=2),
-    # paced persistent forward sweep (counters in the workspace), lags and window counts
-    dict(fwd_sync=1), dict(fwd_sync=1, fwd_sync_lag=4), dict(fwd_sync=1, fwd_rot_windows=5),
-    dict(fwd_sync=1, fwd_two_tables=1), dict(fwd_sync=1, fwd_chunk3=1),
     dict(bwd_accumulator="f64"), dict(bwd_features_per_lane=1), dict(bwd_order=1),
     dict(bwd_unroll=16), dict(bwd_slot_groups=2), dict(bwd_slot_groups=4),
     dict(bwd_lds_bytes=4096), dict(bwd_tasks_per_cu=1), dict(bwd_acc_pad=2), dict(bwd_sel_lds=2),
