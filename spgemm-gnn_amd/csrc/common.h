@@ -112,7 +112,8 @@ struct BwdTask {
   int32_t e1;
   int32_t shared;
   int32_t group;  // selector slot group (packed path): slots [group * k/S, (group+1) * k/S)
-  int32_t pad[2];
+  int32_t chunk;  // row chunk of a shared block (slab flush: chunk 0 -> grad_sp, j -> slab j-1)
+  int32_t pad;
 };
 static_assert(sizeof(BwdTask) == 32, "BwdTask is 2 x dwordx4");
 
@@ -200,9 +201,15 @@ struct maxk_plan {
   int32_t bwd_tp_rows = 1;       // R: destination rows per wavefront of the row pass
   uint32_t* bwd_erec = nullptr;  // [num_edges][2] CSR order: {column, val}
   float* bwd_tbuf = nullptr;     // [num_edges][k] workspace
+  // slab flush of shared blocks (bwd_flush 2): chunk j > 0 of a block stores its partial
+  // into slab j - 1 ([bwd_slabs][num_cols][k] f32 at byte bwd_slab_off of the backward
+  // workspace, behind the selector words), bwd_combine_kernel adds them into grad_sp
+  int32_t bwd_slabs = 0;
+  int64_t bwd_slab_off = 0;
   int64_t device_bytes = 0;
   // per-call scratch: the forward's packed CBSR records (fwd_rec) and the backward's
-  // selector words (bwd_sel) or two-pass product workspace (bwd_tbuf). external_ws: the
+  // selector words + flush slabs (bwd_sel is the base of both) or two-pass product
+  // workspace (bwd_tbuf). external_ws: the
   // plan allocates none of them and the *_ws entry points take the caller's buffer (the
   // Python layer passes one from torch's caching allocator on the launch stream)
   int32_t external_ws = 0;

@@ -344,6 +344,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.external_workspace == 0 || o.external_workspace == 1,
                  "maxk_plan_create: external_workspace must be 0 or 1");
+  MAXK_CHECK_ARG(o.bwd_flush >= 0 && o.bwd_flush <= 2,
+                 "maxk_plan_create: bwd_flush must be 0, 1 or 2");
   maxk_plan* p = new maxk_plan();
   p->external_ws = o.external_workspace;
   p->num_nodes = N;
@@ -818,11 +820,17 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
           t.e1 = co[(size_t)b * (nch + 1) + j + 1];
           t.shared = nch > 1;
           t.group = g;
+          t.chunk = j;
           per_xcd[b % kXcds].push_back(t);
         }
       }
     }
     if (nch > 1) nshared = nblocks;
+    // slab flush (bwd_flush 0/2, the packed kernels): the nch - 1 later chunks of a block
+    // store their partial sums into slabs that one combine pass adds (global float atomics
+    // run at ~1.3 TB/s of added bytes and need a memset grad_sp: an 8-GPU Reddit shard spent
+    // ~10 % of its backward there)
+    if (nch > 1 && packed && o.bwd_flush != 1) p->bwd_slabs = nch - 1;
     size_t len = 0;
     for (auto& v : per_xcd) len = std::max(len, v.size());
     btasks.assign(len * kXcds, BwdTask{});  // padding tasks have ncols == 0
@@ -868,17 +876,21 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, nullptr,
                        p->bwd_row, p->bwd_col, p->bwd_val, E, C, D, p->bwd_rec);
     PLAN_TRY(hipGetLastError());
-    if (p->bwd_feats == 4) {  // per-call lane-ordered selector words (pack_sel_kernel)
-      p->bwd_ws_bytes = (int64_t)std::max(NC, 1) * k;
-      if (!p->external_ws) PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)p->bwd_ws_bytes));
-    }
+    // per-call workspace: lane-ordered selector words (pack_sel_kernel, bwd_feats 4), then
+    // the flush slabs
+    const int64_t sel_bytes = p->bwd_feats == 4 ? (int64_t)std::max(NC, 1) * k : 0;
+    p->bwd_slab_off = (sel_bytes + 255) / 256 * 256;
+    p->bwd_ws_bytes = p->bwd_slabs > 0 ? p->bwd_slab_off + (int64_t)p->bwd_slabs * NC * k * 4
+                                       : sel_bytes;
+    if (p->bwd_ws_bytes > 0 && !p->external_ws)
+      PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)p->bwd_ws_bytes));
     PLAN_TRY(hipStreamSynchronize(s));
     dfree(p->bwd_row);
     dfree(p->bwd_col);
     dfree(p->bwd_val);
     p->bwd_row = p->bwd_col = nullptr;
     p->bwd_val = nullptr;
-    p->device_bytes += (p->bwd_feats == 4 && !p->external_ws ? p->bwd_ws_bytes : 0) +
+    p->device_bytes += (!p->external_ws ? p->bwd_ws_bytes : 0) +
                        12ll * kBwdRecPad;
   }
   PLAN_TRY(hipStreamSynchronize(s));

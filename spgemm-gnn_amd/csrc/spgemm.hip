@@ -499,11 +499,13 @@ template <int U, int NT, bool PF, bool V, bool Q>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
-    float* __restrict__ grad_sp, int k, int S, int ncols_all, int KS, int sel_lds) {
+    float* __restrict__ grad_sp, int k, int S, int ncols_all, int KS, int sel_lds,
+    float* __restrict__ slab) {
   extern __shared__ __align__(16) double bsmem[];
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
-  if (t.ncols == 0 || (t.shared && t.e0 == t.e1)) return;  // padding / nothing to add
+  // padding / nothing to add (with the slab flush every chunk stores its block, zeros too)
+  if (t.ncols == 0 || (t.shared && !slab && t.e0 == t.e1)) return;
   const int ns = k / S;  // slots of this group: [t.group * ns, (t.group + 1) * ns)
   const int L = ns >> 2;  // lanes per edge, 4 slots each: q, q + L, q + 2L, q + 3L
   const int nacc = t.ncols * KS;
@@ -684,13 +686,17 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   }
   __syncthreads();
 
-  float* dst = grad_sp + (size_t)t.col0 * k + t.group * ns;
+  // shared block: global atomics into a zeroed grad_sp, or (slab flush) chunk 0 stores into
+  // grad_sp and chunk j into slab j - 1, summed by bwd_combine_kernel
+  const bool atomic = t.shared && !slab;
+  float* fbase = (slab && t.chunk > 0) ? slab + (size_t)(t.chunk - 1) * ncols_all * k : grad_sp;
+  float* dst = fbase + (size_t)t.col0 * k + t.group * ns;
   const int n = t.ncols * ns;
   for (int i = threadIdx.x; i < n; i += NT) {
     const int c = i / ns;
     const int l = i - c * ns;
     const float a = bacc[c * KS + (V ? (l % L) * 4 + l / L : l)];
-    if (t.shared) global_add(dst + (size_t)c * k + l, a);
+    if (atomic) global_add(dst + (size_t)c * k + l, a);
     else dst[(size_t)c * k + l] = a;
   }
 }
@@ -706,11 +712,12 @@ template <int U, int NT>
 __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint8_t* __restrict__ sp_index,
-    float* __restrict__ grad_sp, int k, int KS) {
+    float* __restrict__ grad_sp, int k, int KS, float* __restrict__ slab, int ncols_all) {
   extern __shared__ __align__(16) double bsmem[];
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
-  if (t.ncols == 0 || (t.shared && t.e0 == t.e1)) return;  // padding / nothing to add
+  // padding / nothing to add (with the slab flush every chunk stores its block, zeros too)
+  if (t.ncols == 0 || (t.shared && !slab && t.e0 == t.e1)) return;
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
   uint8_t* sell = reinterpret_cast<uint8_t*>(bacc + ((nacc + 3) & ~3));
@@ -793,12 +800,44 @@ __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
   }
   __syncthreads();
 
-  float* dst = grad_sp + (size_t)t.col0 * k;
+  const bool atomic = t.shared && !slab;
+  float* base = (slab && t.chunk > 0) ? slab + (size_t)(t.chunk - 1) * ncols_all * k : grad_sp;
+  float* dst = base + (size_t)t.col0 * k;
   for (int i = threadIdx.x; i < nsel; i += NT) {
     const int c = i / k;
     const float a = bacc[c * KS + (i - c * k)];
-    if (t.shared) global_add(dst + i, a);
+    if (atomic) global_add(dst + i, a);
     else dst[i] = a;
+  }
+}
+
+// Slab flush, second step: grad_sp (chunk 0's stores) += slab 0 + slab 1 + ..., in chunk
+// order, so the result does not depend on which work-group finished first.
+__global__ void bwd_combine_kernel(float* __restrict__ grad_sp, const float* __restrict__ slab,
+                                   int nslabs, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((n & 3) == 0) {
+    float4* g4 = reinterpret_cast<float4*>(grad_sp);
+    const float4* s4 = reinterpret_cast<const float4*>(slab);
+    const int64_t n4 = n >> 2;
+    for (int64_t i = t0; i < n4; i += stride) {
+      float4 a = g4[i];
+      for (int j = 0; j < nslabs; ++j) {
+        const float4 b = s4[(size_t)j * n4 + i];
+        a.x += b.x;
+        a.y += b.y;
+        a.z += b.z;
+        a.w += b.w;
+      }
+      g4[i] = a;
+    }
+  } else {
+    for (int64_t i = t0; i < n; i += stride) {
+      float a = grad_sp[i];
+      for (int j = 0; j < nslabs; ++j) a += slab[(size_t)j * n + i];
+      grad_sp[i] = a;
+    }
   }
 }
 
@@ -1271,7 +1310,8 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   if (rc) return rc;
   if (N == 0) return MAXK_OK;
   MAXK_CHECK_ARG(grad_out && sp_index && grad_sp, "maxk_sspmm_backward: null pointer");
-  // per-call scratch: selector words (column kernels) or the E x k products (two-pass)
+  // per-call scratch: selector words + flush slabs (column kernels) or the E x k products
+  // (two-pass)
   uint32_t* sel_ws = plan->bwd_sel;
   float* tbuf_ws = plan->bwd_tbuf;
   if (ws) {
@@ -1283,6 +1323,19 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     set_error("maxk_sspmm_backward: the plan has an external workspace; use maxk_sspmm_backward_ws");
     return MAXK_ERR_INVALID_ARG;
   }
+  float* slab = plan->bwd_slabs > 0
+                    ? reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(sel_ws) + plan->bwd_slab_off)
+                    : nullptr;
+  const int64_t grad_elems = (int64_t)plan->num_cols * k;
+  auto combine = [&]() -> int {
+    if (!slab) return MAXK_OK;
+    const int64_t items = (grad_elems & 3) == 0 ? grad_elems / 4 : grad_elems;
+    const int grid = (int)std::min<int64_t>((items + 255) / 256, 4096);
+    hipLaunchKernelGGL(bwd_combine_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, grad_sp,
+                       slab, plan->bwd_slabs, grad_elems);
+    MAXK_LAUNCH_CHECK("bwd_combine launch");
+    return MAXK_OK;
+  };
   hipStream_t s = (hipStream_t)stream;
   if (plan->bwd_twopass) {
     // the plan checked k % 4 == 0, k / 4 a power of two <= 64, E > 0, NC > 0
@@ -1328,7 +1381,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     MAXK_LAUNCH_CHECK("sspmm_bwd_csc launch");
     return MAXK_OK;
   }
-  if (plan->n_bwd_shared > 0)
+  if (plan->n_bwd_shared > 0 && !slab)  // atomic flush: shared blocks add into zeros
     MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)plan->num_cols * k * sizeof(float), s));
   if (plan->n_bwd_tasks == 0) return MAXK_OK;
   const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k, plan->bwd_acc);
@@ -1342,7 +1395,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       if (lds1 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd1_kernel<UU, NT>, lds1));     \
       hipLaunchKernelGGL((sspmm_bwd1_kernel<UU, NT>), grid, dim3(NT), lds1, s,            \
                          plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sp_index,     \
-                         grad_sp, k, plan->bwd_ks);                                       \
+                         grad_sp, k, plan->bwd_ks, slab, plan->num_cols);                 \
     } while (0)
     const int W = plan->bwd_waves, U = plan->bwd_unroll;
     if (W == 16) BWD1_LAUNCH(16, 1024);
@@ -1354,7 +1407,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     else BWD1_LAUNCH(8, 512);
 #undef BWD1_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd1 launch");
-    return MAXK_OK;
+    return combine();
   }
   if (plan->bwd_rec) {
     const int S = plan->bwd_slot_groups;
@@ -1369,7 +1422,8 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, PF, V, Q>, lds4)); \
       hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF, V, Q>), grid, dim3(NT), lds4, s,  \
                          plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sel_ws, \
-                         grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds); \
+                         grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds,  \
+                         slab);                                                           \
     } while (0)
     const int W = plan->bwd_waves, U = plan->bwd_unroll;
     const bool PFon = plan->bwd_prefetch != 0;
@@ -1407,7 +1461,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     else BWD4_LAUNCH(8, 512, false, false, false);
 #undef BWD4_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd launch");
-    return MAXK_OK;
+    return combine();
   }
 #define BWD_LAUNCH1(F, A, UU)                                                             \
   do {                                                                                    \

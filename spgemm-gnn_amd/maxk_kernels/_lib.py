@@ -87,6 +87,7 @@ class PlanOptions(ctypes.Structure):
         ("fwd_rot_windows", _i32),
         ("fwd_rot_rate", _i32),
         ("external_workspace", _i32),
+        ("bwd_flush", _i32),
     ]
 
 

@@ -389,8 +389,12 @@ PLAN_OPTIONS = [
     dict(bwd_unroll=4), dict(bwd_unroll=12),
     dict(bwd_algo=2), dict(bwd_algo=2, bwd_unroll=4), dict(bwd_algo=3),
     dict(bwd_algo=2, bwd_features_per_lane=1), dict(bwd_algo=2, bwd_features_per_lane=1, bwd_unroll=16),
-    # chunked blocks (atomic flush into a memset grad_sp), both task orders
+    # chunked blocks (slab flush by default, atomic flush into a memset grad_sp with
+    # bwd_flush=1; bwd_order=1 always flushes atomically), both task orders
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=1),
+    dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=2, external_workspace=1),
+    dict(bwd_tasks_per_cu=64, bwd_min_task_edges=16, bwd_features_per_lane=1),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_order=1),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_slot_groups=2),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_accumulator="f64"),
@@ -434,6 +438,30 @@ def test_plan_options_vs_oracle(gpu, opts, k):
     assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref_b, mag_b)
 
 
+@pytest.mark.parametrize("fpl", [4, 1])
+def test_slab_flush_reproducible(gpu, fpl):
+    """Chunked column blocks with the slab flush: the combine adds the chunk partials in
+    chunk order, so two calls agree bitwise (the atomic flush only to the oracle bar), and
+    chunks that hold no edges still store their (zero) block."""
+    p, ix, v = GRAPHS["heavy_split"]()
+    n, d, k = p.size - 1, 256, 16
+    g = graphs.features(n, d, seed=5)
+    od, oi = oracle.maxk(graphs.features(n, d, seed=4).numpy(), k)
+    ref_b, mag_b = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    opts = dict(bwd_tasks_per_cu=64, bwd_min_task_edges=16, bwd_features_per_lane=fpl)
+    plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k, options=opts)
+    info = plan.info()
+    assert info["bwd_shared_blocks"] > 0
+    gi = to_dev(oi, gpu)
+    a = plan.backward(g.to(gpu), gi)
+    b = torch.full_like(a, float("nan"))  # every element must be written
+    plan.backward(g.to(gpu), gi, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert_close(a, ref_b, mag_b)
+
+
 def test_plan_options_rejected(gpu):
     p, ix, v = GRAPHS["single_node"]()
     ptr, idx, val = graph_on(gpu, p, ix, v)
@@ -441,7 +469,8 @@ def test_plan_options_rejected(gpu):
                 dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3),
                 dict(bwd_algo=4), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
                 dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3),
-                dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3), dict(fwd_two_tables=3)):
+                dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3), dict(fwd_two_tables=3),
+                dict(bwd_flush=3)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 
