@@ -112,8 +112,9 @@ struct BwdTask {
   int32_t e1;
   int32_t shared;
   int32_t group;  // selector slot group (packed path): slots [group * k/S, (group+1) * k/S)
-  int32_t chunk;  // row chunk of a shared block (slab flush: chunk 0 -> grad_sp, j -> slab j-1)
-  int32_t pad;
+  int32_t chunk;  // piece index within its block (0 .. pieces - 1)
+  int32_t slab;   // slab flush: float offset of this piece's [C][k] slab region; -1: piece
+                  // 0 (stores straight into grad_sp)
 };
 static_assert(sizeof(BwdTask) == 32, "BwdTask is 2 x dwordx4");
 
@@ -201,11 +202,15 @@ struct maxk_plan {
   int32_t bwd_tp_rows = 1;       // R: destination rows per wavefront of the row pass
   uint32_t* bwd_erec = nullptr;  // [num_edges][2] CSR order: {column, val}
   float* bwd_tbuf = nullptr;     // [num_edges][k] workspace
-  // slab flush of shared blocks (bwd_flush 2): chunk j > 0 of a block stores its partial
-  // into slab j - 1 ([bwd_slabs][num_cols][k] f32 at byte bwd_slab_off of the backward
-  // workspace, behind the selector words), bwd_combine_kernel adds them into grad_sp
-  int32_t bwd_slabs = 0;
+  // slab flush of shared blocks (bwd_flush 2): piece 0 of a block stores into grad_sp,
+  // piece p > 0 into its [C][k] slab region (bwd_slab_floats f32 in all, at byte
+  // bwd_slab_off of the backward workspace, behind the selector words); bwd_combine_kernel
+  // adds each block's regions in piece order. bwd_combine: one int4 {slab offset, regions,
+  // col0, ncols} per block with more than one piece
+  int64_t bwd_slab_floats = 0;
   int64_t bwd_slab_off = 0;
+  int4* bwd_combine = nullptr;
+  int32_t n_bwd_combine = 0;
   int64_t device_bytes = 0;
   // per-call scratch: the forward's packed CBSR records (fwd_rec) and the backward's
   // selector words + flush slabs (bwd_sel is the base of both) or two-pass product

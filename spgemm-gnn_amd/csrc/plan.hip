@@ -214,6 +214,7 @@ static void free_plan(maxk_plan* p) {
   dfree(p->bwd_colptr);
   dfree(p->bwd_erec);
   dfree(p->bwd_tbuf);
+  dfree(p->bwd_combine);
   delete p;
 }
 
@@ -346,6 +347,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: external_workspace must be 0 or 1");
   MAXK_CHECK_ARG(o.bwd_flush >= 0 && o.bwd_flush <= 2,
                  "maxk_plan_create: bwd_flush must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.bwd_piece_edges >= 0, "maxk_plan_create: bwd_piece_edges must be >= 0");
+  MAXK_CHECK_ARG(o.bwd_chunk_bounds >= 0 && o.bwd_chunk_bounds <= 2,
+                 "maxk_plan_create: bwd_chunk_bounds must be 0, 1 or 2");
   maxk_plan* p = new maxk_plan();
   p->external_ws = o.external_workspace;
   p->num_nodes = N;
@@ -780,57 +784,115 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       nch64 = best;
     }
     const int nch = (int)nch64;
-    std::vector<int32_t> rb(nch + 1);
-    for (int j = 0; j <= nch; ++j) {
-      const int64_t target = E * j / nch;
-      rb[j] = (int32_t)(std::lower_bound(hp.begin(), hp.end(), (int32_t)target) - hp.begin());
-    }
-    rb[0] = 0;
-    rb[nch] = N;
-    int32_t *d_rb = nullptr, *d_co = nullptr;
     std::vector<int32_t> co((size_t)nblocks * (nch + 1));
-    auto chunk_cleanup = [&]() { dfree(d_rb); dfree(d_co); };
-#define CH_TRY(x)                                        \
-    do {                                                 \
-      hipError_t e_ = (x);                               \
-      if (e_ != hipSuccess) {                            \
-        chunk_cleanup();                                 \
-        PLAN_TRY(e_);                                    \
-      }                                                  \
-    } while (0)
-    CH_TRY(hipMalloc(&d_rb, sizeof(int32_t) * (nch + 1)));
-    CH_TRY(hipMalloc(&d_co, sizeof(int32_t) * co.size()));
-    CH_TRY(hipMemcpyAsync(d_rb, rb.data(), sizeof(int32_t) * (nch + 1), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(chunk_offsets_kernel, dim3((int)((co.size() + 255) / 256)), dim3(256), 0, s,
-                       p->bwd_row, reinterpret_cast<const int32_t*>(d_offs), nblocks, d_rb,
-                       nch + 1, d_co);
-    CH_TRY(hipGetLastError());
-    CH_TRY(hipMemcpyAsync(co.data(), d_co, sizeof(int32_t) * co.size(), hipMemcpyDeviceToHost, s));
-    CH_TRY(hipStreamSynchronize(s));
-    chunk_cleanup();
+    if (o.bwd_chunk_bounds == 1) {
+      // shared row bounds: chunk j of every block covers the same rows [R_j, R_j+1) (equal
+      // edge counts over the whole graph)
+      std::vector<int32_t> rb(nch + 1);
+      for (int j = 0; j <= nch; ++j) {
+        const int64_t target = E * j / nch;
+        rb[j] = (int32_t)(std::lower_bound(hp.begin(), hp.end(), (int32_t)target) - hp.begin());
+      }
+      rb[0] = 0;
+      rb[nch] = N;
+      int32_t *d_rb = nullptr, *d_co = nullptr;
+      auto chunk_cleanup = [&]() { dfree(d_rb); dfree(d_co); };
+#define CH_TRY(x)                                          \
+      do {                                                 \
+        hipError_t e_ = (x);                               \
+        if (e_ != hipSuccess) {                            \
+          chunk_cleanup();                                 \
+          PLAN_TRY(e_);                                    \
+        }                                                  \
+      } while (0)
+      CH_TRY(hipMalloc(&d_rb, sizeof(int32_t) * (nch + 1)));
+      CH_TRY(hipMalloc(&d_co, sizeof(int32_t) * co.size()));
+      CH_TRY(hipMemcpyAsync(d_rb, rb.data(), sizeof(int32_t) * (nch + 1), hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(chunk_offsets_kernel, dim3((int)((co.size() + 255) / 256)), dim3(256), 0, s,
+                         p->bwd_row, reinterpret_cast<const int32_t*>(d_offs), nblocks, d_rb,
+                         nch + 1, d_co);
+      CH_TRY(hipGetLastError());
+      CH_TRY(hipMemcpyAsync(co.data(), d_co, sizeof(int32_t) * co.size(), hipMemcpyDeviceToHost, s));
+      CH_TRY(hipStreamSynchronize(s));
+      chunk_cleanup();
 #undef CH_TRY
+    } else {
+      // per-block bounds: chunk j of block b holds edges [j, j+1) * nnz_b / nch of the block's
+      // row-sorted stream. On a graph without column locality these are the shared row
+      // bounds to within a few rows (the work-groups that run together still sweep the same
+      // rows of G); with locality (a community linking mostly into its own blocks) every
+      // task keeps an equal share instead of a few tasks carrying most of a chunk
+      // (41-community Reddit-size graph, k = 16: 3.38 -> see DESIGN §6)
+      for (int b = 0; b < nblocks; ++b) {
+        const int64_t o0 = offs[b], nnz = offs[b + 1] - offs[b];
+        for (int j = 0; j <= nch; ++j) co[(size_t)b * (nch + 1) + j] = (int32_t)(o0 + nnz * j / nch);
+      }
+    }
+    // Pieces: a (block, chunk) task holding more than twice the average task's edges is cut
+    // into pieces of equal edge counts (work-groups of their own, in the same chunk-major
+    // slot). The shared row bounds assume edges spread evenly over the blocks; with column
+    // locality (a community of rows linking mostly into its own blocks) a few
+    // tasks would otherwise carry most of a chunk's edges.
+    const int64_t avg_task = std::max<int64_t>(1, E / ((int64_t)nblocks * nch));
+    const int64_t piece_cap = o.bwd_piece_edges > 0 ? (int64_t)o.bwd_piece_edges
+                                                    : std::max<int64_t>(2 * avg_task, 16384);
+    const bool slab_flush = packed && o.bwd_flush != 1;
+    std::vector<int32_t> pieces_of((size_t)nblocks, 0);
+    for (int j = 0; j < nch; ++j)
+      for (int b = 0; b < nblocks; ++b) {
+        const int64_t e = (int64_t)co[(size_t)b * (nch + 1) + j + 1] - co[(size_t)b * (nch + 1) + j];
+        pieces_of[b] += (int32_t)std::max<int64_t>(1, (e + piece_cap - 1) / piece_cap);
+      }
+    // compact slab regions: block b's pieces 1 .. P_b - 1 own C x k floats each
+    std::vector<int64_t> slab_base((size_t)nblocks, -1);
+    std::vector<int4> comb;
+    int64_t slab_floats = 0;
+    for (int b = 0; b < nblocks; ++b) {
+      if (pieces_of[b] > 1) ++nshared;
+      if (slab_flush && pieces_of[b] > 1) {
+        slab_base[b] = slab_floats;
+        const int ncols_b = std::min(C, NC - b * C);
+        comb.push_back(make_int4((int)slab_floats, pieces_of[b] - 1, b * C, ncols_b));
+        slab_floats += (int64_t)(pieces_of[b] - 1) * C * k;
+      }
+    }
+    if (slab_floats >= (int64_t)INT32_MAX) {
+      set_error("maxk_plan_create: backward flush slabs exceed 2^31 floats");
+      return fail(MAXK_ERR_UNSUPPORTED);
+    }
+    std::vector<int32_t> next_piece((size_t)nblocks, 0);
     std::vector<std::vector<BwdTask>> per_xcd(kXcds);
     for (int j = 0; j < nch; ++j) {
       for (int b = 0; b < nblocks; ++b) {
-        for (int g = 0; g < S; ++g) {  // the groups of a block share its edge stream
-          BwdTask t{};
-          t.col0 = b * C;
-          t.ncols = std::min(C, NC - t.col0);
-          t.e0 = co[(size_t)b * (nch + 1) + j];
-          t.e1 = co[(size_t)b * (nch + 1) + j + 1];
-          t.shared = nch > 1;
-          t.group = g;
-          t.chunk = j;
-          per_xcd[b % kXcds].push_back(t);
+        const int32_t e0 = co[(size_t)b * (nch + 1) + j], e1 = co[(size_t)b * (nch + 1) + j + 1];
+        const int np = (int)std::max<int64_t>(1, ((int64_t)e1 - e0 + piece_cap - 1) / piece_cap);
+        for (int q = 0; q < np; ++q) {
+          const int piece = next_piece[b]++;
+          for (int g = 0; g < S; ++g) {  // the groups of a block share its edge stream
+            BwdTask t{};
+            t.col0 = b * C;
+            t.ncols = std::min(C, NC - t.col0);
+            t.e0 = (int32_t)(e0 + ((int64_t)e1 - e0) * q / np);
+            t.e1 = (int32_t)(e0 + ((int64_t)e1 - e0) * (q + 1) / np);
+            t.shared = pieces_of[b] > 1;
+            t.group = g;
+            t.chunk = piece;
+            t.slab = (slab_base[b] >= 0 && piece > 0)
+                         ? (int32_t)(slab_base[b] + (int64_t)(piece - 1) * C * k) : -1;
+            per_xcd[b % kXcds].push_back(t);
+          }
         }
       }
     }
-    if (nch > 1) nshared = nblocks;
-    // slab flush (bwd_flush 0/2, the packed kernels): the nch - 1 later chunks of a block
-    // store their partial sums into slabs that one combine pass adds (global float atomics
-    // run at ~1.3 TB/s of added bytes and need a memset grad_sp: an 8-GPU Reddit shard spent
-    // ~10 % of its backward there)
-    if (nch > 1 && packed && o.bwd_flush != 1) p->bwd_slabs = nch - 1;
+    if (slab_flush && !comb.empty()) {
+      p->bwd_slab_floats = slab_floats;
+      p->n_bwd_combine = (int32_t)comb.size();
+      PLAN_TRY(hipMalloc(&p->bwd_combine, sizeof(int4) * comb.size()));
+      PLAN_TRY(hipMemcpyAsync(p->bwd_combine, comb.data(), sizeof(int4) * comb.size(),
+                              hipMemcpyHostToDevice, s));
+      PLAN_TRY(hipStreamSynchronize(s));
+      p->device_bytes += sizeof(int4) * comb.size();
+    }
     size_t len = 0;
     for (auto& v : per_xcd) len = std::max(len, v.size());
     btasks.assign(len * kXcds, BwdTask{});  // padding tasks have ncols == 0
@@ -880,8 +942,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     // the flush slabs
     const int64_t sel_bytes = p->bwd_feats == 4 ? (int64_t)std::max(NC, 1) * k : 0;
     p->bwd_slab_off = (sel_bytes + 255) / 256 * 256;
-    p->bwd_ws_bytes = p->bwd_slabs > 0 ? p->bwd_slab_off + (int64_t)p->bwd_slabs * NC * k * 4
-                                       : sel_bytes;
+    // flush slabs (bwd_flush 0/2): global float atomics run at ~1.3 TB/s of added bytes and
+    // need a memset grad_sp (an 8-GPU Reddit shard spent ~10 % of its backward there)
+    p->bwd_ws_bytes = p->bwd_slab_floats > 0 ? p->bwd_slab_off + p->bwd_slab_floats * 4
+                                             : sel_bytes;
     if (p->bwd_ws_bytes > 0 && !p->external_ws)
       PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)p->bwd_ws_bytes));
     PLAN_TRY(hipStreamSynchronize(s));

@@ -686,11 +686,11 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   }
   __syncthreads();
 
-  // shared block: global atomics into a zeroed grad_sp, or (slab flush) chunk 0 stores into
-  // grad_sp and chunk j into slab j - 1, summed by bwd_combine_kernel
+  // shared block: global atomics into a zeroed grad_sp, or (slab flush) piece 0 stores into
+  // grad_sp and piece p > 0 into its slab region, summed by bwd_combine_kernel
   const bool atomic = t.shared && !slab;
-  float* fbase = (slab && t.chunk > 0) ? slab + (size_t)(t.chunk - 1) * ncols_all * k : grad_sp;
-  float* dst = fbase + (size_t)t.col0 * k + t.group * ns;
+  float* dst = (slab && t.slab >= 0) ? slab + t.slab + t.group * ns
+                                     : grad_sp + (size_t)t.col0 * k + t.group * ns;
   const int n = t.ncols * ns;
   for (int i = threadIdx.x; i < n; i += NT) {
     const int c = i / ns;
@@ -712,7 +712,7 @@ template <int U, int NT>
 __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint8_t* __restrict__ sp_index,
-    float* __restrict__ grad_sp, int k, int KS, float* __restrict__ slab, int ncols_all) {
+    float* __restrict__ grad_sp, int k, int KS, float* __restrict__ slab) {
   extern __shared__ __align__(16) double bsmem[];
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
@@ -801,8 +801,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
   __syncthreads();
 
   const bool atomic = t.shared && !slab;
-  float* base = (slab && t.chunk > 0) ? slab + (size_t)(t.chunk - 1) * ncols_all * k : grad_sp;
-  float* dst = base + (size_t)t.col0 * k;
+  float* dst = (slab && t.slab >= 0) ? slab + t.slab : grad_sp + (size_t)t.col0 * k;
   for (int i = threadIdx.x; i < nsel; i += NT) {
     const int c = i / k;
     const float a = bacc[c * KS + (i - c * k)];
@@ -811,32 +810,35 @@ __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
   }
 }
 
-// Slab flush, second step: grad_sp (chunk 0's stores) += slab 0 + slab 1 + ..., in chunk
-// order, so the result does not depend on which work-group finished first.
-__global__ void bwd_combine_kernel(float* __restrict__ grad_sp, const float* __restrict__ slab,
-                                   int nslabs, int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if ((n & 3) == 0) {
-    float4* g4 = reinterpret_cast<float4*>(grad_sp);
-    const float4* s4 = reinterpret_cast<const float4*>(slab);
-    const int64_t n4 = n >> 2;
-    for (int64_t i = t0; i < n4; i += stride) {
-      float4 a = g4[i];
-      for (int j = 0; j < nslabs; ++j) {
-        const float4 b = s4[(size_t)j * n4 + i];
+// Slab flush, second step: one work-group per block with several pieces adds the block's
+// slab regions (piece 1, 2, ... in order) into grad_sp, which piece 0 stored, so the result
+// does not depend on which work-group finished first. comb[i] = {float offset of the block's
+// first region, regions, col0, ncols}; regions are region_floats = C * k apart.
+__global__ __launch_bounds__(256) void bwd_combine_kernel(float* __restrict__ grad_sp,
+                                                          const float* __restrict__ slab,
+                                                          const int4* __restrict__ comb, int k,
+                                                          int region_floats) {
+  const int4 cb = comb[blockIdx.x];
+  const int n = cb.w * k;
+  float* g = grad_sp + (size_t)cb.z * k;
+  const float* sl = slab + cb.x;
+  if ((k & 3) == 0) {
+    for (int i = threadIdx.x * 4; i < n; i += 256 * 4) {
+      float4 a = *reinterpret_cast<const float4*>(g + i);
+      for (int j = 0; j < cb.y; ++j) {
+        const float4 b = *reinterpret_cast<const float4*>(sl + (size_t)j * region_floats + i);
         a.x += b.x;
         a.y += b.y;
         a.z += b.z;
         a.w += b.w;
       }
-      g4[i] = a;
+      *reinterpret_cast<float4*>(g + i) = a;
     }
   } else {
-    for (int64_t i = t0; i < n; i += stride) {
-      float a = grad_sp[i];
-      for (int j = 0; j < nslabs; ++j) a += slab[(size_t)j * n + i];
-      grad_sp[i] = a;
+    for (int i = threadIdx.x; i < n; i += 256) {
+      float a = g[i];
+      for (int j = 0; j < cb.y; ++j) a += sl[(size_t)j * region_floats + i];
+      g[i] = a;
     }
   }
 }
@@ -1323,16 +1325,14 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     set_error("maxk_sspmm_backward: the plan has an external workspace; use maxk_sspmm_backward_ws");
     return MAXK_ERR_INVALID_ARG;
   }
-  float* slab = plan->bwd_slabs > 0
+  float* slab = plan->bwd_slab_floats > 0
                     ? reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(sel_ws) + plan->bwd_slab_off)
                     : nullptr;
-  const int64_t grad_elems = (int64_t)plan->num_cols * k;
   auto combine = [&]() -> int {
     if (!slab) return MAXK_OK;
-    const int64_t items = (grad_elems & 3) == 0 ? grad_elems / 4 : grad_elems;
-    const int grid = (int)std::min<int64_t>((items + 255) / 256, 4096);
-    hipLaunchKernelGGL(bwd_combine_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, grad_sp,
-                       slab, plan->bwd_slabs, grad_elems);
+    hipLaunchKernelGGL(bwd_combine_kernel, dim3(plan->n_bwd_combine), dim3(256), 0,
+                       (hipStream_t)stream, grad_sp, slab, plan->bwd_combine, k,
+                       plan->bwd_block_cols * k);
     MAXK_LAUNCH_CHECK("bwd_combine launch");
     return MAXK_OK;
   };
@@ -1395,7 +1395,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       if (lds1 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd1_kernel<UU, NT>, lds1));     \
       hipLaunchKernelGGL((sspmm_bwd1_kernel<UU, NT>), grid, dim3(NT), lds1, s,            \
                          plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sp_index,     \
-                         grad_sp, k, plan->bwd_ks, slab, plan->num_cols);                 \
+                         grad_sp, k, plan->bwd_ks, slab);                                 \
     } while (0)
     const int W = plan->bwd_waves, U = plan->bwd_unroll;
     if (W == 16) BWD1_LAUNCH(16, 1024);

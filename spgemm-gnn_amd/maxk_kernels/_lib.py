@@ -88,6 +88,8 @@ class PlanOptions(ctypes.Structure):
         ("fwd_rot_rate", _i32),
         ("external_workspace", _i32),
         ("bwd_flush", _i32),
+        ("bwd_piece_edges", _i32),
+        ("bwd_chunk_bounds", _i32),
     ]
 
 

@@ -82,6 +82,47 @@ def synthetic_csr(num_nodes: int, num_edges: int, seed: int = 97, sigma: float =
     return ptr.to(torch.int32), cols.to(torch.int32)
 
 
+def community_csr(num_nodes: int, num_edges: int, communities: int = 41, p_in: float = 0.76,
+                  seed: int = 97, sigma: float = 1.2, shuffle: bool = False, device="cpu"):
+    """A locality-bearing variant of :func:`synthetic_csr` (supplementary measurements only,
+    DESIGN §6): the same lognormal row degrees, but each edge's column is drawn, with
+    probability ``p_in``, uniformly inside the row's community and otherwise uniformly over
+    all nodes. Communities are contiguous ID blocks of ~N/communities nodes. The defaults
+    follow the Reddit dataset: 41 subreddit classes and an edge homophily of about 0.76.
+    Duplicate columns are merged, so E comes out slightly below ``num_edges``; one self-loop
+    per row. ``shuffle``: relabel the nodes by a seeded random permutation. That keeps the
+    community structure but hides it from ID order, as a dataset's arbitrary node ids do.
+    Returns (ptr int32 [N+1], idx int32 [E]) with sorted columns."""
+    device = torch.device(device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    n = int(num_nodes)
+    c = max(1, min(int(communities), n))
+    deg = lognormal_degrees(n, int(num_edges) - n, sigma, gen, device)
+    m = int(deg.sum())
+    rows = torch.repeat_interleave(torch.arange(n, device=device), deg)
+    size = -(-n // c)
+    lo = (rows // size) * size
+    width = torch.clamp(n - lo, max=size)
+    u = torch.rand(m, generator=gen, device=device, dtype=torch.float64)
+    inside = torch.rand(m, generator=gen, device=device) < p_in
+    cols = torch.where(inside, lo + (u * width.to(torch.float64)).to(torch.int64),
+                       (u * n).to(torch.int64))
+    cols = torch.minimum(cols, torch.full_like(cols, n - 1))
+    ar = torch.arange(n, device=device)
+    rows = torch.cat([rows, ar])
+    cols = torch.cat([cols, ar])
+    if shuffle:
+        perm = torch.randperm(n, generator=gen, device=device)
+        rows, cols = perm[rows], perm[cols]
+    key = torch.unique(rows * n + cols)  # sorted, duplicates merged
+    rows = key // n
+    cols = key - rows * n
+    ptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    ptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+    return ptr.to(torch.int32), cols.to(torch.int32)
+
+
 def row_degrees(ptr: torch.Tensor) -> torch.Tensor:
     return (ptr[1:] - ptr[:-1]).to(torch.int64)
 

@@ -153,6 +153,10 @@ GRAPHS = {
                                         graphs.sage_mean_values(p).numpy()))(
         *graphs.synthetic_csr(5000, 120_000, seed=31)),
     "heavy_split": heavy_graph,
+    # community structure in ID order (column locality): GCN values
+    "community": lambda: (lambda p, i: (p.numpy(), i.numpy(),
+                                        graphs.gcn_values(p, i).numpy()))(
+        *graphs.community_csr(6000, 150_000, communities=12, seed=33)),
     "empty_rows": empty_rows_graph,
     "single_node": lambda: (np.array([0, 1], np.int32), np.array([0], np.int32),
                             np.array([0.5], np.float32)),
@@ -395,6 +399,14 @@ PLAN_OPTIONS = [
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=1),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=2, external_workspace=1),
     dict(bwd_tasks_per_cu=64, bwd_min_task_edges=16, bwd_features_per_lane=1),
+    # pieces: every (block, chunk) task cut into pieces of <= 500 edges (slab regions per
+    # piece), with chunks, slot groups, the one-slot kernel and the atomic flush
+    dict(bwd_piece_edges=500), dict(bwd_piece_edges=500, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_piece_edges=500, bwd_slot_groups=2), dict(bwd_piece_edges=500, bwd_features_per_lane=1),
+    dict(bwd_piece_edges=500, bwd_flush=1),
+    # chunk bounds shared by every block (the per-block equal-edge bounds are the default)
+    dict(bwd_chunk_bounds=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_chunk_bounds=1, bwd_piece_edges=500),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_order=1),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_slot_groups=2),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_accumulator="f64"),
@@ -470,7 +482,7 @@ def test_plan_options_rejected(gpu):
                 dict(bwd_algo=4), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
                 dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3),
                 dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3), dict(fwd_two_tables=3),
-                dict(bwd_flush=3)):
+                dict(bwd_flush=3), dict(bwd_piece_edges=-1), dict(bwd_chunk_bounds=3)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 
