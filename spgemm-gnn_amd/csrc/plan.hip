@@ -339,8 +339,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: fwd_record_bytes must be 0 or a multiple of 16 >= 5k");
   MAXK_CHECK_ARG(o.fwd_chunk3 >= 0 && o.fwd_chunk3 <= 2, "maxk_plan_create: fwd_chunk3 must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_features_per_lane == 0 || o.bwd_features_per_lane == 1 ||
+                     (o.bwd_features_per_lane == 2 && k % 2 == 0) ||
                      (o.bwd_features_per_lane == 4 && k % 4 == 0),
-                 "maxk_plan_create: bwd_features_per_lane must be 0, 1 or 4 (k % 4 == 0)");
+                 "maxk_plan_create: bwd_features_per_lane must be 0, 1, 2 (k % 2 == 0) or 4 (k % 4 == 0)");
   MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
                  "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.external_workspace == 0 || o.external_workspace == 1,
@@ -381,8 +382,11 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   }
   p->fwd_acc = o.fwd_accumulator ? o.fwd_accumulator : MAXK_ACC_F64;
   p->bwd_acc = o.bwd_accumulator ? o.bwd_accumulator : MAXK_ACC_F32_CAS;
+  // k = 8: two slots per lane, so a gather instruction still covers 16 edges (4 lanes per
+  // edge) instead of 32 edges of ~8 rows (Reddit k = 8: 1.230 -> 1.173 ms with unroll 12)
   p->bwd_feats = o.bwd_features_per_lane ? o.bwd_features_per_lane
-                                         : (k % 4 == 0 ? 4 : 1);
+                                         : (k == 8 ? 2 : (k % 4 == 0 ? 4 : 1));
+  if (p->bwd_feats == 2 && o.bwd_unroll == 0) p->bwd_unroll = 12;
 
   int32_t* row_of = nullptr;
   uint32_t* keys_in = nullptr;
@@ -592,7 +596,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // packed path (sspmm_bwd4_kernel): f32 accumulators, 4 selector slots per lane, grad_out
   // addressable with 32-bit byte offsets
   // (or sspmm_bwd1_kernel: one slot per lane, k <= 64 lanes per edge)
-  const bool packed = E > 0 && ((k % 4 == 0 && p->bwd_feats == 4) || (p->bwd_feats == 1 && k <= kWave)) &&
+  const bool packed = E > 0 &&
+                      ((k % 4 == 0 && p->bwd_feats == 4) || (k % 2 == 0 && p->bwd_feats == 2 && k / 2 <= kWave) ||
+                       (p->bwd_feats == 1 && k <= kWave)) &&
                       p->bwd_acc == MAXK_ACC_F32_CAS &&
                       (uint64_t)N * (uint64_t)D * 4u <= 0xffffffffull;
   // Slot groups: the k selector slots are split into S groups of k/S consecutive (sorted,
@@ -600,16 +606,16 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // few grad_out lines its group's features fall in, and a block spans S times more
   // columns, so more edges share each fetched row (SSpMM is bound by L1-miss requests).
   int S = 1;
-  if (packed && p->bwd_feats == 4) {
+  if (packed && (p->bwd_feats == 4 || p->bwd_feats == 2)) {
     S = o.bwd_slot_groups ? o.bwd_slot_groups : kBwdSlotGroups;
-    while (S > 1 && (k % (4 * S)) != 0) S >>= 1;
+    while (S > 1 && (k % (p->bwd_feats * S)) != 0) S >>= 1;
   }
   p->bwd_slot_groups = S;
   const int nslots = k / S;
   // accumulator row stride: nslots + 1 (odd: columns start on different banks) or nslots
   // 64-bit CAS pairs (sspmm_bwd4_kernel<.., V>): KS even, unpadded by default
   // (Reddit k = 16: 2.06 -> 1.78 ms; k = 8 1.24 -> 1.16; k = 32 3.21 -> 3.09)
-  p->bwd_cas64 = packed && p->bwd_feats == 4 && o.bwd_cas64 != 2;
+  p->bwd_cas64 = packed && (p->bwd_feats == 4 || p->bwd_feats == 2) && o.bwd_cas64 != 2;
   // (Reddit bwd k = 16 1.76 -> 1.70 ms, k = 32 3.08 -> 2.93, k = 64 5.43 -> 4.86; the forward's
   // 8-B edge words gain nothing: forward only on request)
   p->bwd_quad = o.quad_loads != 2;
@@ -629,7 +635,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // 10-43 % vs 2 % for CSC, 7.0 vs 8.0 L2 misses per edge); a column's in-edges come from
   // anywhere. Kept as an option for that comparison.
   const int Lc = k / p->bwd_feats;  // lanes per edge of the column-major kernel
-  const bool csc_ok = E > 0 && k % p->bwd_feats == 0 && (Lc & (Lc - 1)) == 0 && Lc <= kWave &&
+  const bool csc_ok = E > 0 && p->bwd_feats != 2 && k % p->bwd_feats == 0 && (Lc & (Lc - 1)) == 0 &&
+                      Lc <= kWave &&
                       (uint64_t)N * (uint64_t)D * 4u <= 0xffffffffull;
   p->bwd_csc = csc_ok && o.bwd_algo == 2;
   // Two-pass backward (bwd_algo = 3; auto when a column block would see each grad_out row it
@@ -940,7 +947,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     PLAN_TRY(hipGetLastError());
     // per-call workspace: lane-ordered selector words (pack_sel_kernel, bwd_feats 4), then
     // the flush slabs
-    const int64_t sel_bytes = p->bwd_feats == 4 ? (int64_t)std::max(NC, 1) * k : 0;
+    const int64_t sel_bytes = (p->bwd_feats == 4 || p->bwd_feats == 2) ? (int64_t)std::max(NC, 1) * k : 0;
     p->bwd_slab_off = (sel_bytes + 255) / 256 * 256;
     // flush slabs (bwd_flush 0/2): global float atomics run at ~1.3 TB/s of added bytes and
     // need a memset grad_sp (an 8-GPU Reddit shard spent ~10 % of its backward there)

@@ -25,6 +25,7 @@
 //             float pairs; the block is stored (or atomically flushed when it is split over
 //             several work-groups) once at the end.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -487,15 +488,34 @@ __global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int n, int
            ((uint32_t)s[3 * L] << 24);
 }
 
+// Two slots per lane (sspmm_bwd4_kernel<.., F = 2>): sel[(g * n + c) * L + q] = slots
+// g*k/S + q and g*k/S + q + L of column c (L = k / 2S), as one u16.
+__global__ void pack_sel2_kernel(const uint8_t* __restrict__ sp_index, int n, int k, int S,
+                                 uint16_t* __restrict__ sel) {
+  const int L = k / (2 * S);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * L * S) return;
+  const int g = i / (n * L);
+  const int r = i - g * (n * L);
+  const int c = r / L, q = r - c * L;
+  const uint8_t* s = sp_index + (size_t)c * k + g * (k / S) + q;
+  sel[i] = (uint16_t)(s[0] | (s[L] << 8));
+}
+
 // NT threads per work-group (8, 12 or 16 waves: more waves, more gathers in flight per CU
 // under the same LDS block). PF: the next sub-steps' records are loaded right after this
 // step's gathers are issued, so the record stream's HBM latency overlaps the LDS updates
 // (loads retire in issue order, so they must not precede the gathers the updates wait on).
 //
-// V (plan->bwd_cas64): lane q's 4 slots are stored adjacently (slot l of a column at
-// (l % L) * 4 + l / L), so its updates are 1 ds_read_b128 + 2 ds_cmpst_rtn_b64 instead of
-// 4 + 4 dword operations (KS % 4 == 0); a pair is retried if either of its floats changed.
-template <int U, int NT, bool PF, bool V, bool Q>
+// V (plan->bwd_cas64): lane q's F slots are stored adjacently (slot l of a column at
+// (l % L) * F + l / L), so its updates are 1 ds_read_b128 + 2 ds_cmpst_rtn_b64 (F = 4) or
+// 1 ds_read_b64 + 1 ds_cmpst_rtn_b64 (F = 2) instead of F + F dword operations (KS % F == 0);
+// a pair is retried if either of its floats changed.
+//
+// F: selector slots per lane, L = k / (F S) lanes per edge. F = 4: a gather instruction
+// covers slots 4i..4i+3 (a quarter of the sorted selectors) of 64/L edges; F = 2: slots
+// 8i..8i+7 of half as many edges, so of about half as many rows of G.
+template <int U, int NT, bool PF, bool V, bool Q, int F = 4>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
@@ -506,15 +526,17 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const BwdTask t = tasks[blockIdx.x];
   // padding / nothing to add (with the slab flush every chunk stores its block, zeros too)
   if (t.ncols == 0 || (t.shared && !slab && t.e0 == t.e1)) return;
+  static_assert(F == 2 || F == 4, "2 or 4 slots per lane");
+  using SelT = std::conditional_t<F == 4, uint32_t, uint16_t>;  // the F selectors of a lane
   const int ns = k / S;  // slots of this group: [t.group * ns, (t.group + 1) * ns)
-  const int L = ns >> 2;  // lanes per edge, 4 slots each: q, q + L, q + 2L, q + 3L
+  const int L = ns / F;  // lanes per edge, F slots each: q, q + L, ...
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
   // sel_lds: the block's selector words are staged in LDS behind the accumulator, so the
   // per-edge selector lookup is an LDS read instead of an L1 miss (the G rows evict the
   // block's 16 B/column table from the 32 KB L1)
-  const uint32_t* selg = sel + ((size_t)t.group * ncols_all + t.col0) * L;
-  uint32_t* sell = reinterpret_cast<uint32_t*>(bacc) + ((nacc + 3) & ~3);
+  const SelT* selg = reinterpret_cast<const SelT*>(sel) + ((size_t)t.group * ncols_all + t.col0) * L;
+  SelT* sell = reinterpret_cast<SelT*>(bacc + ((nacc + 3) & ~3));
   if (sel_lds)
     for (int i = threadIdx.x; i < t.ncols * L; i += NT) sell[i] = selg[i];
   __syncthreads();
@@ -529,8 +551,8 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const int stride = kWaves * EPS * U;
   const __amdgpu_buffer_rsrc_t gr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
-  const uint32_t* selb = (sel_lds ? sell : selg) + q;
-  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + (V ? 4 * q : q);
+  const SelT* selb = (sel_lds ? sell : selg) + q;
+  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + (V ? F * q : q);
   const uint3* rec3 = reinterpret_cast<const uint3*>(rec);
 
   // records past e1 (a padded or neighbouring record) are loaded and ignored
@@ -568,11 +590,11 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     uint32_t s[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) s[u] = selb[cl[u] * L];
-    float x[U][4];
+    float x[U][F];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < F; ++i) {
         const uint32_t off = go[u] + (((s[u] >> (8 * i)) & 0xffu) << 2);
         x[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
       }
@@ -587,28 +609,33 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) x[u][i] *= v[u];
+      for (int i = 0; i < F; ++i) x[u][i] *= v[u];
     if constexpr (V) {
       using u64 = unsigned long long;
-      u64 old2[U][2];
+      u64 old2[U][F / 2];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        // one ds_read_b128 (KS % 4 == 0); a stale value only costs a CAS retry
-        const uint4 o4 = *reinterpret_cast<const uint4*>(accq + cl[u] * KS);
-        old2[u][0] = (u64)o4.x | ((u64)o4.y << 32);
-        old2[u][1] = (u64)o4.z | ((u64)o4.w << 32);
+        // one ds_read_b128 / b64 (KS % F == 0); a stale value only costs a CAS retry
+        if constexpr (F == 4) {
+          const uint4 o4 = *reinterpret_cast<const uint4*>(accq + cl[u] * KS);
+          old2[u][0] = (u64)o4.x | ((u64)o4.y << 32);
+          old2[u][1] = (u64)o4.z | ((u64)o4.w << 32);
+        } else {
+          const uint2 o2 = *reinterpret_cast<const uint2*>(accq + cl[u] * KS);
+          old2[u][0] = (u64)o2.x | ((u64)o2.y << 32);
+        }
       }
       auto addp = [](u64 o, float a0, float a1) -> u64 {
         const float lo = __uint_as_float((unsigned)o) + a0;
         const float hi = __uint_as_float((unsigned)(o >> 32)) + a1;
         return (u64)__float_as_uint(lo) | ((u64)__float_as_uint(hi) << 32);
       };
-      u64 got2[U][2];
+      u64 got2[U][F / 2];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < F / 2; ++h) {
           got2[u][h] = old2[u][h];
           if (ok[u]) {
             u64 expected = old2[u][h];
@@ -624,7 +651,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
       for (int u = 0; u < U; ++u) {
         u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < F / 2; ++h) {
           if (ok[u] && got2[u][h] != old2[u][h]) {
             u64 cur = got2[u][h];
             while (true) {
@@ -641,20 +668,20 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
       }
       continue;
     }
-    unsigned old[U][4];
+    unsigned old[U][F];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       unsigned* a = accq + cl[u] * KS;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < F; ++i)
         old[u][i] = __hip_atomic_load(a + i * L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    unsigned got[U][4];
+    unsigned got[U][F];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       unsigned* a = accq + cl[u] * KS;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < F; ++i) {
         got[u][i] = old[u][i];
         if (ok[u]) {
           unsigned expected = old[u][i];
@@ -669,7 +696,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     for (int u = 0; u < U; ++u) {
       unsigned* a = accq + cl[u] * KS;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < F; ++i) {
         if (ok[u] && got[u][i] != old[u][i]) {
           unsigned cur = got[u][i];
           while (true) {
@@ -695,7 +722,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   for (int i = threadIdx.x; i < n; i += NT) {
     const int c = i / ns;
     const int l = i - c * ns;
-    const float a = bacc[c * KS + (V ? (l % L) * 4 + l / L : l)];
+    const float a = bacc[c * KS + (V ? (l % L) * F + l / L : l)];
     if (atomic) global_add(dst + (size_t)c * k + l, a);
     else dst[(size_t)c * k + l] = a;
   }
@@ -1407,6 +1434,44 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     else BWD1_LAUNCH(8, 512);
 #undef BWD1_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd1 launch");
+    return combine();
+  }
+  if (plan->bwd_rec && plan->bwd_feats == 2) {  // two slots per lane
+    const int S = plan->bwd_slot_groups;
+    const int nsel = plan->num_cols * (k / 2);
+    hipLaunchKernelGGL(pack_sel2_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
+                       plan->num_cols, k, S, reinterpret_cast<uint16_t*>(sel_ws));
+    const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
+    const size_t lds2 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
+                        (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
+#define BWD2_LAUNCH(UU, NT, V, Q)                                                         \
+    do {                                                                                  \
+      if (lds2 > 64 * 1024)                                                               \
+        MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, false, V, Q, 2>, lds2));         \
+      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, false, V, Q, 2>), grid, dim3(NT), lds2, s, \
+                         plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sel_ws,       \
+                         grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds,  \
+                         slab);                                                           \
+    } while (0)
+    const int U = plan->bwd_unroll;
+    const bool QL = plan->bwd_quad && (k / S / 2) % 4 == 0;
+    if (plan->bwd_cas64) {
+      if (U >= 16) {
+        if (QL) BWD2_LAUNCH(16, 512, true, true);
+        else BWD2_LAUNCH(16, 512, true, false);
+      } else if (U >= 12) {
+        if (QL) BWD2_LAUNCH(12, 512, true, true);
+        else BWD2_LAUNCH(12, 512, true, false);
+      } else {
+        if (QL) BWD2_LAUNCH(8, 512, true, true);
+        else BWD2_LAUNCH(8, 512, true, false);
+      }
+    } else {
+      if (QL) BWD2_LAUNCH(8, 512, false, true);
+      else BWD2_LAUNCH(8, 512, false, false);
+    }
+#undef BWD2_LAUNCH
+    MAXK_LAUNCH_CHECK("sspmm_bwd2 launch");
     return combine();
   }
   if (plan->bwd_rec) {

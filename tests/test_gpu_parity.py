@@ -404,6 +404,11 @@ PLAN_OPTIONS = [
     dict(bwd_piece_edges=500), dict(bwd_piece_edges=500, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
     dict(bwd_piece_edges=500, bwd_slot_groups=2), dict(bwd_piece_edges=500, bwd_features_per_lane=1),
     dict(bwd_piece_edges=500, bwd_flush=1),
+    # two slots per lane (k/2 lanes per edge): unrolls, slot groups, dword CAS, chunks
+    dict(bwd_features_per_lane=2), dict(bwd_features_per_lane=2, bwd_unroll=12),
+    dict(bwd_features_per_lane=2, bwd_unroll=16), dict(bwd_features_per_lane=2, bwd_slot_groups=2),
+    dict(bwd_features_per_lane=2, bwd_cas64=2), dict(bwd_features_per_lane=2, quad_loads=2),
+    dict(bwd_features_per_lane=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
     # chunk bounds shared by every block (the per-block equal-edge bounds are the default)
     dict(bwd_chunk_bounds=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
     dict(bwd_chunk_bounds=1, bwd_piece_edges=500),
