@@ -382,10 +382,19 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   }
   p->fwd_acc = o.fwd_accumulator ? o.fwd_accumulator : MAXK_ACC_F64;
   p->bwd_acc = o.bwd_accumulator ? o.bwd_accumulator : MAXK_ACC_F32_CAS;
-  // k = 8: two slots per lane, so a gather instruction still covers 16 edges (4 lanes per
-  // edge) instead of 32 edges of ~8 rows (Reddit k = 8: 1.230 -> 1.173 ms with unroll 12)
+  // k = 8: two slots per lane, so a gather instruction covers 16 edges (4 lanes per edge)
+  // instead of 32, when a column block sees few edges per grad_out row (32 edges then span
+  // ~4 rows: Reddit, 7.7 edges per (block, row), 1.151 -> 1.125 ms with unroll 12); with
+  // more (ogbn-proteins, 15) the 32 edges share ~2 rows and 4 slots per lane stay faster
+  // (0.831 vs 0.877 ms). Edges per (block, row) estimated from the LDS budget.
+  bool two_slots = false;
+  if (k == 8 && N > 0 && NC > 0) {
+    const int lds0 = o.bwd_lds_bytes ? o.bwd_lds_bytes : kBwdLdsBudget;
+    const double c0 = std::min<double>(NC, (lds0 - 16) / (5.0 * k));
+    two_slots = (double)E / N * c0 / NC < 10.0;
+  }
   p->bwd_feats = o.bwd_features_per_lane ? o.bwd_features_per_lane
-                                         : (k == 8 ? 2 : (k % 4 == 0 ? 4 : 1));
+                                         : (two_slots ? 2 : (k % 4 == 0 ? 4 : 1));
   if (p->bwd_feats == 2 && o.bwd_unroll == 0) p->bwd_unroll = 12;
 
   int32_t* row_of = nullptr;

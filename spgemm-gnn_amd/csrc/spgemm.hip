@@ -837,20 +837,24 @@ __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
   }
 }
 
-// Slab flush, second step: one work-group per block with several pieces adds the block's
-// slab regions (piece 1, 2, ... in order) into grad_sp, which piece 0 stored, so the result
-// does not depend on which work-group finished first. comb[i] = {float offset of the block's
-// first region, regions, col0, ncols}; regions are region_floats = C * k apart.
+// Slab flush, second step: the blocks with several pieces add their slab regions (piece 1, 2,
+// ... in order) into grad_sp, which piece 0 stored, so the result does not depend on which
+// work-group finished first. comb[blockIdx.y] = {float offset of the block's first region,
+// regions, col0, ncols}; regions are region_floats = C * k apart; blockIdx.x picks a slice of
+// kCombineSlice floats of the block (one work-group per block was 40 work-groups on
+// ogbn-proteins at k = 8, about 50 us).
+constexpr int kCombineSlice = 1024;
 __global__ __launch_bounds__(256) void bwd_combine_kernel(float* __restrict__ grad_sp,
                                                           const float* __restrict__ slab,
                                                           const int4* __restrict__ comb, int k,
                                                           int region_floats) {
-  const int4 cb = comb[blockIdx.x];
-  const int n = cb.w * k;
+  const int4 cb = comb[blockIdx.y];
+  const int n = min(cb.w * k, (int)(blockIdx.x + 1) * kCombineSlice);
+  const int i0 = blockIdx.x * kCombineSlice;
   float* g = grad_sp + (size_t)cb.z * k;
   const float* sl = slab + cb.x;
   if ((k & 3) == 0) {
-    for (int i = threadIdx.x * 4; i < n; i += 256 * 4) {
+    for (int i = i0 + threadIdx.x * 4; i < n; i += 256 * 4) {
       float4 a = *reinterpret_cast<const float4*>(g + i);
       for (int j = 0; j < cb.y; ++j) {
         const float4 b = *reinterpret_cast<const float4*>(sl + (size_t)j * region_floats + i);
@@ -862,7 +866,7 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(float* __restrict__ gr
       *reinterpret_cast<float4*>(g + i) = a;
     }
   } else {
-    for (int i = threadIdx.x; i < n; i += 256) {
+    for (int i = i0 + threadIdx.x; i < n; i += 256) {
       float a = g[i];
       for (int j = 0; j < cb.y; ++j) a += sl[(size_t)j * region_floats + i];
       g[i] = a;
@@ -1357,7 +1361,8 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
                     : nullptr;
   auto combine = [&]() -> int {
     if (!slab) return MAXK_OK;
-    hipLaunchKernelGGL(bwd_combine_kernel, dim3(plan->n_bwd_combine), dim3(256), 0,
+    const int slices = (plan->bwd_block_cols * k + kCombineSlice - 1) / kCombineSlice;
+    hipLaunchKernelGGL(bwd_combine_kernel, dim3(slices, plan->n_bwd_combine), dim3(256), 0,
                        (hipStream_t)stream, grad_sp, slab, plan->bwd_combine, k,
                        plan->bwd_block_cols * k);
     MAXK_LAUNCH_CHECK("bwd_combine launch");
