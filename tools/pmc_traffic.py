@@ -25,7 +25,7 @@ from collections import defaultdict
 
 CALLS = 4  # tools/pmc_driver.py: 1 + 3 calls per direction
 FWD = ("pack_cbsr_kernel", "pack_cbsr3_kernel", "zero_rows_kernel", "spgemm_fwd_kernel")
-BWD_PACK = ("pack_sel_kernel",)
+BWD_PACK = ("pack_sel_kernel", "pack_sel2_kernel", "bwd_combine_kernel")  # per-call, beside the SSpMM
 
 
 def family(name):
