@@ -872,9 +872,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
         slab_floats += (int64_t)(pieces_of[b] - 1) * C * k;
       }
     }
-    if (slab_floats >= (int64_t)INT32_MAX) {
-      set_error("maxk_plan_create: backward flush slabs exceed 2^31 floats");
-      return fail(MAXK_ERR_UNSUPPORTED);
+    if (slab_floats >= (int64_t)INT32_MAX) {  // task offsets are int32: flush atomically
+      comb.clear();
+      slab_floats = 0;
+      std::fill(slab_base.begin(), slab_base.end(), -1);
     }
     std::vector<int32_t> next_piece((size_t)nblocks, 0);
     std::vector<std::vector<BwdTask>> per_xcd(kXcds);
