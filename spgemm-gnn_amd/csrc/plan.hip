@@ -767,15 +767,16 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   if (colsort) {
     // no tasks: the column-major kernels run one wave per column
   } else if (xcd_order && E > 0 && nblocks > 0) {
-    // Row-chunk-major, XCD-aware order. Chunk j of every block covers the same rows
-    // [R_j, R_j+1) (equal edge counts over the whole graph), so the work-groups that run
-    // together sweep the same rows of G and share its lines in their XCD's L2. Work-groups
-    // are dealt round-robin over the 8 XCDs (blockIdx % 8 labels the work-groups sharing an
-    // XCD; speed only, correctness never depends on it): XCD x owns blocks b = x (mod 8)
-    // and walks (chunk, block) in chunk-major order.
-    // every chunk task flushes its whole block (C * k atomics) however few edges it has:
-    // keep >= kBwdMinTaskEdges edges per task (a row shard of a multi-GPU partition has
-    // 1/W of the edges over the same blocks)
+    // Row-chunk-major, XCD-aware order. Chunk j of a block is the j-th equal share of its
+    // row-sorted edge stream (below), so on graphs without column locality chunk j of every
+    // block covers about the same rows and the work-groups that run together sweep the same
+    // rows of G, sharing its lines in their XCD's L2. Work-groups are dealt round-robin over
+    // the 8 XCDs (blockIdx % 8 labels the work-groups sharing an XCD; speed only, correctness
+    // never depends on it): XCD x owns blocks b = x (mod 8) and walks (chunk, block) in
+    // chunk-major order.
+    // every chunk task clears and flushes its whole block (C * k floats) however few edges
+    // it has: keep >= kBwdMinTaskEdges edges per task (a row shard of a multi-GPU partition
+    // has 1/W of the edges over the same blocks)
     // ... but not fewer tasks than CUs while those keep >= 16k edges (a row shard of an
     // 8-GPU partition: 256 tasks of ~56k edges ran 0.24 ms, 512 of ~28k 0.27, 128 0.40)
     int64_t nch64 = std::min<int64_t>(chunks, E / ((int64_t)nblocks * min_task_edges));
