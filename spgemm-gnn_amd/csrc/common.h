@@ -47,7 +47,8 @@ constexpr double kFwdPackedTableBytes16 = 32e6;
 // 1.70 / 5.35; ogbn-proteins k = 8 (15) 0.94 / 2.68
 constexpr double kBwdTwoPassReuse = 0.75;
 constexpr int kBwdRowsPerWave = 4;  // row pass: most destination rows one wavefront stages
-constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (S = 2, 4 measured slower)
+constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (plan: 2 at k >= 32 with
+                                     // few edges per block row)
 // Records past the end of the backward edge list that a wave may read (and ignore).
 constexpr int kBwdRecPad = (kBwdThreads / kWave) * kWave * 16 + kWave;  // MI355X: 8 XCDs, work-groups dealt round-robin (speed only)
 constexpr int kBwdLdsBudget = 160 * 1024; // all of a CU's LDS: one 512-thread work-group per CU

@@ -617,6 +617,14 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   int S = 1;
   if (packed && (p->bwd_feats == 4 || p->bwd_feats == 2)) {
     S = o.bwd_slot_groups ? o.bwd_slot_groups : kBwdSlotGroups;
+    if (o.bwd_slot_groups == 0 && p->bwd_feats == 4 && k >= 32 && k % 8 == 0 && N > 0 && NC > 0) {
+      // k >= 32 with few edges per (block, row): two slot groups, i.e. k/8 lanes per edge and
+      // blocks of twice the columns (Reddit, ~1.9 edges per block row at k = 32: 2.88 ->
+      // 2.66 ms; k = 64, ~1.0: 4.88 -> 4.71; ogbn-proteins k = 64, ~1.9: 3.32 -> 3.25). With
+      // more reuse one group stays faster (ogbn-proteins k = 32, ~3.1: 1.82 vs 1.86).
+      const double c1 = std::min<double>(NC, (lds_budget - 16) / (5.0 * k));
+      if ((double)E / N * c1 / NC < 2.5) S = 2;
+    }
     while (S > 1 && (k % (p->bwd_feats * S)) != 0) S >>= 1;
   }
   p->bwd_slot_groups = S;
