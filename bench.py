@@ -170,6 +170,9 @@ def main():
     ap.add_argument("--no-comparator", action="store_true")
     ap.add_argument("--k-sweep", default="8,32,64",
                     help="extra k values timed at N=1 (kernel device time; '' to skip)")
+    ap.add_argument("--graph", default="auto",
+                    help="'synthetic', 'auto' (the DGL cache file ~/.dgl/... when it exists, "
+                         "else synthetic) or a path to a scipy save_npz adjacency")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -186,11 +189,27 @@ def main():
     n, e_target = graphs.DATASETS[args.dataset]
     d, k = args.dim, args.k
     t0 = time.perf_counter()
-    ptr, idx = graphs.synthetic_csr(n, e_target, seed=97, device=dev)
+    gpath = None
+    if args.graph == "auto":
+        gpath = graphs.find_dgl_graph(args.dataset)
+    elif args.graph != "synthetic":
+        gpath = args.graph
+    if gpath:
+        ptr, idx = graphs.load_npz_csr(gpath, device=dev)
+        n = ptr.numel() - 1
+        data = (f"graph loaded from {gpath} (+ self-loops); N(0,1) features seed 97, "
+                f"upstream grad seed 98")
+    else:
+        ptr, idx = graphs.synthetic_csr(n, e_target, seed=97, device=dev)
+        data = (f"synthetic ({args.dataset}-shaped graph: lognormal degrees sigma=1.2, uniform "
+                f"columns, self-loops, seed 97; N(0,1) features seed 97, upstream grad seed 98)")
     val = graphs.sage_mean_values(ptr)
     e = idx.numel()
     torch.cuda.synchronize()
-    log(f"graph {args.dataset}: N={n} E={e} generated in {time.perf_counter() - t0:.1f}s")
+    log(f"graph {args.dataset}: N={n} E={e} {'loaded' if gpath else 'generated'} in "
+        f"{time.perf_counter() - t0:.1f}s")
+    # PMC traffic in --traffic-json was collected on the synthetic graphs
+    tkey = args.dataset if not gpath else args.dataset + ":file"
 
     part = RowPartition(ptr, world, phases=args.phases if world > 1 else 1)
     r0, r1 = part.rows(rank)
@@ -284,7 +303,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            key = f"{args.dataset}:k{k}:d{d}:n{world}"
+            key = f"{tkey}:k{k}:d{d}:n{world}"
             traffic = tj.get(key, {}).get(dom)
             detail = tj.get(key, {}).get(dom + "_detail", {})
         except (OSError, ValueError):
@@ -302,8 +321,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (Reddit-shaped graph: lognormal degrees sigma=1.2, uniform "
-                "columns, self-loops, seed 97; N(0,1) features seed 97, upstream grad seed 98)",
+        "data": data,
         "config": {
             "workload": f"{args.dataset} SpGEMM fwd + SSpMM bwd over CBSR (MaxK exact), "
                         f"D={d}, k={k}",
@@ -352,7 +370,7 @@ def main():
         bytes (traffic well above the compulsory bytes = re-reads)."""
         ent = {}
         try:
-            ent = json.load(open(args.traffic_json)).get(f"{args.dataset}:k{ks}:d{d}:n1", {})
+            ent = json.load(open(args.traffic_json)).get(f"{tkey}:k{ks}:d{d}:n1", {})
         except (OSError, ValueError):
             pass
         out = {}

@@ -153,6 +153,59 @@ def features(num_nodes: int, dim: int, seed: int, device="cpu",
     return torch.randn(num_nodes, dim, generator=g, device=gd).to(device)
 
 
+# DGL's on-disk dataset cache (``dgl.data.RedditDataset`` et al.): <root>/<dir>/<file>. The
+# graph file is a scipy.sparse ``save_npz`` archive of the symmetric adjacency, without
+# self-loops. Used by bench.py when it exists on the box.
+DGL_GRAPH_FILES = {"reddit": ("reddit", "reddit_graph.npz")}
+
+
+def find_dgl_graph(name: str, root: Optional[str] = None) -> Optional[str]:
+    """Path of the DGL cache file for dataset ``name`` if it exists, else None."""
+    import os
+    if name not in DGL_GRAPH_FILES:
+        return None
+    root = root or os.environ.get("DGL_DOWNLOAD_DIR") or os.path.expanduser("~/.dgl")
+    sub, fname = DGL_GRAPH_FILES[name]
+    path = os.path.join(root, sub, fname)
+    return path if os.path.isfile(path) else None
+
+
+def load_npz_csr(path: str, self_loops: bool = True, device="cpu"):
+    """Destination-row CSR (ptr int32 [N+1], idx int32 [E], sorted columns) from a
+    scipy.sparse ``save_npz`` archive (COO or CSR/CSC). Read with ``numpy.load`` and
+    ``allow_pickle=False``: nothing in the file is executed. Edge (u, v) of the archive is
+    DGL's edge u -> v, so destination row v lists its sources u (DGL's in-edge CSR,
+    ``adj_tensors('csc')``). ``self_loops`` appends one (v, v) per node, as DGL's
+    ``AddSelfLoop`` does (run/reddit.log:28 counts 114,848,857 edges after it)."""
+    import numpy as np
+    with np.load(path, allow_pickle=False) as z:
+        fmt = z["format"].item()
+        fmt = fmt.decode() if isinstance(fmt, bytes) else str(fmt)
+        shape = tuple(int(x) for x in z["shape"])
+        if fmt == "coo":
+            src, dst = z["row"].astype(np.int64), z["col"].astype(np.int64)
+        elif fmt in ("csr", "csc"):
+            indptr, indices = z["indptr"].astype(np.int64), z["indices"].astype(np.int64)
+            major = np.repeat(np.arange(indptr.size - 1, dtype=np.int64), np.diff(indptr))
+            src, dst = (major, indices) if fmt == "csr" else (indices, major)
+        else:
+            raise ValueError(f"{path}: unsupported sparse format {fmt!r}")
+    if shape[0] != shape[1]:
+        raise ValueError(f"{path}: adjacency must be square, got {shape}")
+    n = shape[0]
+    rows = torch.from_numpy(dst).to(device)
+    cols = torch.from_numpy(src).to(device)
+    if self_loops:
+        ar = torch.arange(n, device=rows.device)
+        rows, cols = torch.cat([rows, ar]), torch.cat([cols, ar])
+    key, _ = torch.sort(rows * n + cols)
+    rows = key // n
+    cols = key - rows * n
+    ptr = torch.zeros(n + 1, dtype=torch.int64, device=rows.device)
+    ptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+    return ptr.to(torch.int32), cols.to(torch.int32)
+
+
 def dataset_csr(name: str, device="cpu", seed: int = 97):
     n, e = DATASETS[name]
     return synthetic_csr(n, e, seed=seed, device=device)

@@ -48,3 +48,33 @@ def test_community_csr_deterministic():
     a = graphs.community_csr(2000, 40_000, seed=9)
     b = graphs.community_csr(2000, 40_000, seed=9)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def test_load_npz_csr_coo_and_csr(tmp_path):
+    """scipy save_npz adjacency (the DGL dataset cache format) -> destination-row CSR with
+    self-loops: row v lists the sources u of edges u -> v."""
+    import numpy as np
+    import scipy.sparse as sps
+    rng = np.random.default_rng(4)
+    n, m = 500, 4000
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    keep = src != dst
+    src, dst = src[keep], dst[keep]
+    key = np.unique(dst * n + src)
+    dst, src = key // n, key % n
+    coo = sps.coo_matrix((np.ones(src.size, np.float32), (src, dst)), shape=(n, n))
+    ref = sps.csr_matrix((np.ones(src.size + n), (np.r_[dst, np.arange(n)], np.r_[src, np.arange(n)])),
+                         shape=(n, n))
+    ref.sort_indices()
+    for i, mat in enumerate((coo, coo.tocsr(), coo.tocsc())):
+        path = tmp_path / f"g{i}.npz"
+        sps.save_npz(path, mat)
+        ptr, idx = graphs.load_npz_csr(str(path))
+        _check_csr(ptr, idx, n)
+        assert np.array_equal(ptr.numpy(), ref.indptr)
+        assert np.array_equal(idx.numpy(), ref.indices)
+    assert graphs.find_dgl_graph("reddit", root=str(tmp_path)) is None
+    (tmp_path / "reddit").mkdir()
+    sps.save_npz(tmp_path / "reddit" / "reddit_graph.npz", coo)
+    assert graphs.find_dgl_graph("reddit", root=str(tmp_path)).endswith("reddit_graph.npz")
