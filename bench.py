@@ -181,10 +181,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # MAXK_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks sharing the GPUs
+    # a one-GPU box has (collectives staged through host memory; timings not meaningful)
+    backend = os.environ.get("MAXK_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"MAXK_BENCH_BACKEND={backend}: expected nccl or gloo")
+    dev_index = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     n, e_target = graphs.DATASETS[args.dataset]
     d, k = args.dim, args.k
@@ -328,7 +337,8 @@ def main():
             "dataset": args.dataset, "num_nodes": n, "num_edges": e, "dim_origin": d,
             "dim_k": k,
             "parallelism": "single-gpu" if world == 1 else
-            f"row-partition x{world} + RCCL all-gather(CBSR) / reduce-scatter(grad_sp)",
+            f"row-partition x{world} + {'RCCL' if backend == 'nccl' else 'gloo (rehearsal)'} "
+            f"all-gather(CBSR) / reduce-scatter(grad_sp)",
         },
         "roofline": {
             "bound": "hbm",
