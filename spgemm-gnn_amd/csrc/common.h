@@ -152,6 +152,11 @@ struct maxk_plan {
   int32_t fwd_acc = MAXK_ACC_F64;
   int32_t fwd_rec_bytes = 0;     // packed CBSR record size (k % 4 == 0)
   uint8_t* fwd_rec = nullptr;    // [num_cols][fwd_rec_bytes] workspace (per call pack)
+  // fixed-point forward (LdsFix): per task {sexp, gexp} (fwd_fix_stats_kernel); the call's
+  // {max |x|, min |x|} words live at fwd_xstat_off of the forward workspace
+  int32_t fwd_fixed = 0;
+  int2* fwd_fix = nullptr;
+  int64_t fwd_xstat_off = 0;
   maxk::FwdTask* fwd_tasks = nullptr;   // e0/e1 index the permuted edge order below
   int32_t fwd_phases = 1;        // column phases per forward call
   int32_t fwd_persistent = 0;    // grid = resident capacity (1) or one work-group per task

@@ -94,6 +94,46 @@ __global__ void gather_fwd_kernel(const int32_t* __restrict__ perm,
   }
 }
 
+// Fixed-point forward bounds per task (spgemm.hip, fwd_fix_scale): one work-group per task
+// over its edge words. sexp: every row of the task has sum |val| <= 2^sexp over the task's
+// edges (f32 sums, with 2^-10 of headroom for their rounding); gexp = sexp - vexp with every
+// nonzero |val| >= 2^vexp. Non-finite values force the f64 path (gexp = 1000).
+__global__ __launch_bounds__(256) void fwd_fix_stats_kernel(const FwdTask* __restrict__ tasks,
+                                                            const uint2* __restrict__ cv,
+                                                            int2* __restrict__ out) {
+  __shared__ float rsum[kFwdMaxTileRows];
+  __shared__ uint32_t vmin_bits, bad;
+  const FwdTask t = tasks[blockIdx.x];
+  for (int i = threadIdx.x; i < kFwdMaxTileRows; i += blockDim.x) rsum[i] = 0.f;
+  if (threadIdx.x == 0) { vmin_bits = 0x7fffffffu; bad = 0u; }
+  __syncthreads();
+  uint32_t mn = 0x7fffffffu;
+  for (int e = t.e0 + (int)threadIdx.x; e < t.e1; e += blockDim.x) {
+    const uint2 w = cv[e];
+    const uint32_t b = w.y & 0x7fffffffu;
+    if (b >= 0x7f800000u) bad = 1u;
+    if (b) mn = min(mn, b);
+    atomicAdd(&rsum[w.x >> kFwdColBits], __uint_as_float(b));
+  }
+  atomicMin(&vmin_bits, mn);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float smax = 0.f;
+    for (int i = 0; i < kFwdMaxTileRows; ++i) smax = fmaxf(smax, rsum[i]);
+    int2 r = make_int2(0, 0);
+    if (bad || !(smax < 3.0e38f)) {
+      r.y = 1000;
+    } else if (smax > 0.f && vmin_bits != 0x7fffffffu) {
+      int es = 0, ev = 0;
+      (void)frexpf(smax * (1.0f + 0x1p-10f), &es);  // smax * (1 + 2^-10) < 2^es
+      (void)frexpf(__uint_as_float(vmin_bits), &ev);  // vmin >= 2^(ev - 1)
+      r.x = es;
+      r.y = es - (ev - 1);
+    }
+    out[blockIdx.x] = r;
+  }
+}
+
 // Sort key of each edge for the backward: its source-column block c / C (a stable radix
 // sort then yields the block-major, destination-row-sorted edge list). Also validates the
 // column ids: any idx outside [0, NC) sets *bad (the compute kernels index the CBSR tables
@@ -202,6 +242,7 @@ static void free_plan(maxk_plan* p) {
   dfree(p->fwd_rec);
   dfree(p->fwd_perm);
   dfree(p->fwd_cv);
+  dfree(p->fwd_fix);
   dfree(p->fwd_phase_off);
   dfree(p->zero_rows);
   dfree(p->bwd_tasks);
@@ -286,6 +327,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   MAXK_CHECK_ARG(o.fwd_accumulator >= 0 && o.fwd_accumulator <= MAXK_ACC_F32_CAS &&
                      o.bwd_accumulator >= 0 && o.bwd_accumulator <= MAXK_ACC_F32_CAS,
                  "maxk_plan_create: unknown accumulator kind");
+  MAXK_CHECK_ARG(o.fwd_fixed >= 0 && o.fwd_fixed <= 2,
+                 "maxk_plan_create: fwd_fixed must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_lds_bytes >= 0 && o.bwd_lds_bytes <= 160 * 1024 &&
                      o.bwd_tasks_per_cu >= 0 && o.fwd_task_cap >= 0 && o.fwd_phases >= 0 &&
                      o.bwd_min_task_edges >= 0 &&
@@ -381,6 +424,18 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       p->cus = prop.multiProcessorCount;
   }
   p->fwd_acc = o.fwd_accumulator ? o.fwd_accumulator : MAXK_ACC_F64;
+  // Fixed-point forward (LdsFix; the packed 4-values-per-lane and lane-chunk kernels with the
+  // f64 kind). Measured (tools/fwd_fixed_sweep.py, fixed vs f64 ms): Reddit k = 16 1.22 / 1.34,
+  // k = 24 1.57 / 1.95, k = 32 1.80 / 2.46, k = 64 3.45 / 4.81; ogbn-proteins k = 16 0.80 / 0.93,
+  // k = 64 2.22 / 3.37. Not by default at k < 16 (Reddit k = 8 0.93 / 0.91, the stats pass
+  // included) or on tables past the packed-record thresholds, whose gathers are HBM-bound
+  // (ogbn-products k = 16 3.14 / 3.02, k = 32 4.86 / 4.78).
+  {
+    const bool big = (double)std::max(NC, 1) * 5.0 * k >
+                     (k >= 32 ? kFwdPackedTableBytes : kFwdPackedTableBytes16);
+    p->fwd_fixed = (o.fwd_fixed == 1 || (o.fwd_fixed == 0 && k >= 16 && !big)) &&
+                   p->fwd_acc == MAXK_ACC_F64 && (k % 4 == 0 || p->fwd_chunk3);
+  }
   p->bwd_acc = o.bwd_accumulator ? o.bwd_accumulator : MAXK_ACC_F32_CAS;
   // k = 8: two slots per lane, so a gather instruction covers 16 edges (4 lanes per edge)
   // instead of 32, when a column block sees few edges per grad_out row (32 edges then span
@@ -519,6 +574,13 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     PLAN_TRY(hipMemcpyAsync(p->fwd_tasks, ftasks.data(), sizeof(FwdTask) * ftasks.size(),
                             hipMemcpyHostToDevice, s));
     p->device_bytes += sizeof(FwdTask) * ftasks.size();
+    if (p->fwd_fixed) {
+      PLAN_TRY(hipMalloc(&p->fwd_fix, sizeof(int2) * ftasks.size()));
+      p->device_bytes += sizeof(int2) * ftasks.size();
+      hipLaunchKernelGGL(fwd_fix_stats_kernel, dim3((int)ftasks.size()), dim3(256), 0, s,
+                         p->fwd_tasks, p->fwd_cv, p->fwd_fix);
+      PLAN_TRY(hipGetLastError());
+    }
     // Column windows. Default: one launch whose tiles start their column-sorted sweep at the
     // window a shared clock points to (fwd_rot_ticks per window, about one tile's duration
     // per full turn), so the tiles running together on an XCD gather from nearby columns
@@ -582,6 +644,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   } else if (k % 4 == 0 && NC > 0) {
     p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes : cbsr_record_bytes(k);
     p->fwd_ws_bytes = (int64_t)NC * p->fwd_rec_bytes;
+  }
+  if (p->fwd_fix) {  // the call's {max |x|, min |x|} words after the records
+    p->fwd_xstat_off = (p->fwd_ws_bytes + 255) / 256 * 256;
+    p->fwd_ws_bytes = p->fwd_xstat_off + 256;
   }
   if (p->fwd_ws_bytes > 0 && !p->external_ws) {  // plan-owned per-call pack buffer
     PLAN_TRY(hipMalloc(&p->fwd_rec, (size_t)p->fwd_ws_bytes));
@@ -1014,6 +1080,9 @@ extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* st
     hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
                        (hipStream_t)stream, p->fwd_perm, nullptr, nullptr, val, p->num_edges,
                        p->fwd_cv, false);
+  if (p->fwd_fix && p->n_fwd_tasks > 0)
+    hipLaunchKernelGGL(fwd_fix_stats_kernel, dim3(p->n_fwd_tasks), dim3(256), 0,
+                       (hipStream_t)stream, p->fwd_tasks, p->fwd_cv, p->fwd_fix);
   MAXK_LAUNCH_CHECK("maxk_plan_refresh_values launch");
   return MAXK_OK;
 }

@@ -47,17 +47,24 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
 }
 
 
+// add(p, v): one accumulated term. The forward's edge loop uses scale(val, sc) once per edge
+// and add2(p, scaled val, x) per slot, so the fixed-point accumulator below can fold the scale
+// and the rounding into one fma.
 template <>
 struct LdsAcc<MAXK_ACC_F64> {
   using T = double;
+  using V = float;
   static __device__ __forceinline__ void add(double* p, float v) {
     lds_add(p, (double)v);
   }
+  static __device__ __forceinline__ V scale(float v, double) { return v; }
+  static __device__ __forceinline__ void add2(double* p, float v, float x) { add(p, v * x); }
 };
 
 template <>
 struct LdsAcc<MAXK_ACC_F32_CAS> {
   using T = float;
+  using V = float;
   static __device__ __forceinline__ void add(float* p, float v) {
     unsigned* u = reinterpret_cast<unsigned*>(p);
     unsigned old = *u;
@@ -67,7 +74,97 @@ struct LdsAcc<MAXK_ACC_F32_CAS> {
       if (old == assumed) break;
     }
   }
+  static __device__ __forceinline__ V scale(float v, double) { return v; }
+  static __device__ __forceinline__ void add2(float* p, float v, float x) { add(p, v * x); }
 };
+
+// Forward fixed-point accumulator (plan->fwd_fixed): ds_add_u64 runs at ~1.9x the ds_add_f64
+// rate, and the f64 atomic bounds the forward at k >= 32 (tools/probe_fwd_build.py: Reddit
+// k = 32 2.46 -> 1.74 ms, k = 64 4.79 -> 3.34 with the integer atomic). A term val * x is
+// scaled by 2^s (per task and call, fwd_fix_scale) and rounded to an integer by ONE fma with
+// M = 1.5 * 2^52: r = fma(val * 2^s, x, M) lies in [2^52, 2^53) while |term| < 2^51, where the
+// f64 bit pattern of r is bits(M) + round(term). The slot accumulates these raw patterns
+// (mod 2^64); bits(M) = 0x867 * 2^51 vanishes mod 2^51, so the low 51 bits, read as a signed
+// residue, are the exact integer sum as long as |sum| < 2^50 (fwd_fix_decode). The products
+// are exact in f64 (24 x 24 bits) and the integer sum is exact, so the only error is the one
+// rounding per term, at most 2^-(s+1).
+struct LdsFix {
+  using T = unsigned long long;
+  using V = double;
+  static __device__ __forceinline__ V scale(float v, double sc) { return (double)v * sc; }
+  static __device__ __forceinline__ void add2(T* p, double v, float x) {
+    const double r = __builtin_fma(v, (double)x, 0x1.8p52);
+    __hip_atomic_fetch_add(p, (T)__double_as_longlong(r), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+};
+
+__device__ __forceinline__ double fwd_fix_decode(unsigned long long a, double inv) {
+  const long long t = (long long)(a << 13) >> 13;  // low 51 bits as a signed residue
+  return (double)t * inv;
+}
+
+// Per task and call: the scale 2^s of the fixed-point forward, or 0 (use f64). fix = {sexp,
+// gexp} from fwd_fix_stats_kernel: every row of the task has sum |val| <= 2^sexp, and every
+// nonzero |val| >= 2^(sexp - gexp). xs = {max |x| bits, 0x7fffffff - min nonzero |x| bits}
+// over the call's sp_data (fwd_xstat_kernel). With 2^ex > max |x| and min |x| >= 2^en:
+// s = 49 - sexp - ex keeps every row's sum of |terms| below 2^49; the rounding error of a term,
+// 2^-(s+1), relative to the smallest possible nonzero term 2^(sexp - gexp + en), is at most
+// 2^(gexp + ex - en - 50). The fixed path is taken when that is <= 2^-25, so every output
+// whose terms do not cancel (|y| >= sum |terms| / 2) is within 2^-24 relative, the rounding of
+// the f32 result itself. Non-finite or all-zero inputs take the f64 path.
+__device__ __forceinline__ double fwd_fix_scale(int2 fix, const uint32_t* xs) {
+  const uint32_t mx = xs[0];
+  const uint32_t mn = 0x7fffffffu - xs[32];
+  if (mx == 0u || mx >= 0x7f800000u || mn == 0u || mn > mx) return 0.0;
+  const int ex = (int)(mx >> 23) - 126;                      // max |x| < 2^ex
+  const int en = (mn >> 23) ? (int)(mn >> 23) - 127 : -149;  // min |x| >= 2^en
+  if (fix.y + ex - en > 25) return 0.0;
+  const int sc = 49 - fix.x - ex;
+  if (sc > 1000 || sc < -1000) return 0.0;
+  return __builtin_ldexp(1.0, sc);
+}
+
+// max |x| and min nonzero |x| of the call's sp_data (bit patterns of non-negative floats
+// order like integers). st[0] (max) and st[32] (0x7fffffff - min) sit on different cache
+// lines and are zeroed before the launch; a few hundred work-groups reduce in LDS and add
+// one atomic each per word (one atomic per wave on a shared word cost ~190 us at k = 16).
+__global__ __launch_bounds__(256) void fwd_xstat_kernel(const float* __restrict__ x, int64_t n,
+                                                        uint32_t* st) {
+  __shared__ uint32_t smx[256 / kWave], smn[256 / kWave];
+  uint32_t mx = 0u, mn = 0x7fffffffu;
+  const int64_t n4 = n / 4;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = x4[i];
+    const uint32_t b[4] = {__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu,
+                           __float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mx = max(mx, b[j]);
+      mn = min(mn, b[j] ? b[j] : 0x7fffffffu);
+    }
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t b = __float_as_uint(x[i]) & 0x7fffffffu;
+    mx = max(mx, b);
+    if (b) mn = min(mn, b);
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+  }
+  const int w = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0) { smx[w] = mx; smn[w] = mn; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 256 / kWave; ++i) { mx = max(mx, smx[i]); mn = min(mn, smn[i]); }
+    atomicMax(&st[0], mx);
+    atomicMax(&st[32], 0x7fffffffu - mn);
+  }
+}
 
 // --------------------------------------------------------------------------------------
 // forward
@@ -134,7 +231,8 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
                                            int nwaves, int EPS, int slot, int l0, bool lane_on,
                                            const uint2* __restrict__ cv,
                                            const uint8_t* __restrict__ rec, int rec_bytes,
-                                           const uint8_t* __restrict__ seltab, int D, int k) {
+                                           const uint8_t* __restrict__ seltab, int D, int k,
+                                           double sc) {
   using T = typename A::T;
   constexpr bool PF = (FL & kFwdFlagPrefetch) != 0;
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
@@ -203,17 +301,17 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
       if ((FL & kFwdFlagBranchless) || ok[u]) {
         T* arow = acc + (cw[u] >> kFwdColBits) * D;
         const uint32_t sv = sel[u];
-        const float vu = (FL & kFwdFlagBranchless) && !ok[u] ? 0.f : v[u];
+        const typename A::V vu = A::scale((FL & kFwdFlagBranchless) && !ok[u] ? 0.f : v[u], sc);
         if constexpr (C3) {
           // l0 = chunk index: slots 3 l0 .. 3 l0 + 2 (the last chunk may be partly padding)
-          A::add(arow + (sv & 0xffu), vu * x[u].x);
-          if (3 * l0 + 1 < k) A::add(arow + ((sv >> 8) & 0xffu), vu * x[u].y);
-          if (3 * l0 + 2 < k) A::add(arow + ((sv >> 16) & 0xffu), vu * x[u].z);
+          A::add2(arow + (sv & 0xffu), vu, x[u].x);
+          if (3 * l0 + 1 < k) A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
+          if (3 * l0 + 2 < k) A::add2(arow + ((sv >> 16) & 0xffu), vu, x[u].z);
         } else {
-          A::add(arow + (sv & 0xffu), vu * x[u].x);
-          A::add(arow + ((sv >> 8) & 0xffu), vu * x[u].y);
-          A::add(arow + ((sv >> 16) & 0xffu), vu * x[u].z);
-          A::add(arow + (sv >> 24), vu * x[u].w);
+          A::add2(arow + (sv & 0xffu), vu, x[u].x);
+          A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
+          A::add2(arow + ((sv >> 16) & 0xffu), vu, x[u].z);
+          A::add2(arow + (sv >> 24), vu, x[u].w);
         }
       }
     }
@@ -230,7 +328,8 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     int phases, int phase, const uint2* __restrict__ cv,
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
     const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
-    int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab, int accum) {
+    int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab, int accum,
+    const int2* __restrict__ fix_tab, const uint32_t* __restrict__ xstat) {
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
@@ -259,6 +358,13 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   t.e1 = phase_off[ti * (phases + 1) + phase + 1];
   }
   if ((phase > 0 || accum) && t.e0 == t.e1) continue;  // nothing to add (uniform)
+  // fixed-point accumulation for this task (LdsFix), else f64; the 8-byte slots are the same
+  double fsc = 0.0;
+  if constexpr (VEC == 4 && ACC == MAXK_ACC_F64) {
+    if (fix_tab && !(phase > 0 || accum)) fsc = fwd_fix_scale(fix_tab[ti], xstat);
+  }
+  const bool fixed = fsc != 0.0;
+  unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(smem_d);
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
   const int n = nrows * D;
@@ -292,14 +398,23 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     // chain (col, val) -> CBSR record -> LDS has two dependent global round trips, so
     // memory-level parallelism comes from U independent sub-steps per wave. Out-of-range
     // lanes load a clamped (valid) edge and skip the update.
-    if (emid >= 0) {
-      fwd_edges4<U, A, FL>(acc, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, seltab, DS, k);
-      fwd_edges4<U, A, FL>(acc, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, seltab, DS, k);
+    auto sweep = [&](auto* a, auto tag) {
+      using AA = decltype(tag);
+      if (emid >= 0) {
+        fwd_edges4<U, AA, FL>(a, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+                              rec_bytes, seltab, DS, k, fsc);
+        fwd_edges4<U, AA, FL>(a, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+                              rec_bytes, seltab, DS, k, fsc);
+      } else {
+        fwd_edges4<U, AA, FL>(a, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+                              rec_bytes, seltab, DS, k, fsc);
+      }
+    };
+    if constexpr (ACC == MAXK_ACC_F64) {
+      if (fixed) sweep(acc64, LdsFix{});
+      else sweep(acc, A{});
     } else {
-      fwd_edges4<U, A, FL>(acc, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                           rec_bytes, seltab, DS, k);
+      sweep(acc, A{});
     }
   } else {
     for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
@@ -317,8 +432,10 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   __syncthreads();
 
   float* dst = out + (size_t)t.row0 * D;
+  const double finv = fixed ? 1.0 / fsc : 0.0;  // 2^-s, exact
   auto get = [&](int i) -> float {
     const int r = i / D;
+    if (fixed) return (float)fwd_fix_decode(acc64[r * DS + (i - r * D)], finv);
     return (float)acc[r * DS + (i - r * D)];
   };
   if (!split) {
@@ -1215,6 +1332,18 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
                        rec_ws, plan->num_cols, k, rec_bytes);
     MAXK_LAUNCH_CHECK("pack_cbsr launch");
   }
+  // fixed-point forward: the call's max / min |x| for fwd_fix_scale (one pass over sp_data)
+  const int2* fix_tab = nullptr;
+  uint32_t* xstat = nullptr;
+  if (plan->fwd_fix && !accum && plan->num_cols > 0) {
+    fix_tab = plan->fwd_fix;
+    xstat = reinterpret_cast<uint32_t*>(ws_base + plan->fwd_xstat_off);
+    MAXK_HIP_TRY(hipMemsetAsync(xstat, 0, 256, s));
+    const int64_t nx = (int64_t)plan->num_cols * k;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nx + 4095) / 4096, 2 * plan->cus));
+    hipLaunchKernelGGL(fwd_xstat_kernel, dim3(grid), dim3(256), 0, s, sp_data, nx, xstat);
+    MAXK_LAUNCH_CHECK("fwd_xstat launch");
+  }
   const int rot = plan->fwd_rot_ticks;
   // persistent grid: as many work-groups as fit on the device at once (capped by tasks)
 #define FWD_LAUNCH1(V, A, UU, NT, FL)                                                     \
@@ -1230,7 +1359,7 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU, NT, FL>), dim3(g), dim3(NT), lds, s, \
                          plan->fwd_tasks, plan->n_fwd_tasks, plan->fwd_phase_off, B, b,   \
                          plan->fwd_cv, sp_data, sp_index, recp,                           \
-                         rec_bytes_eff, out, D, k, R, rot, seltab, accum);                \
+                         rec_bytes_eff, out, D, k, R, rot, seltab, accum, fix_tab, xstat); \
   } while (0)
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \

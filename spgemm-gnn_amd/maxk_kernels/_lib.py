@@ -90,6 +90,7 @@ class PlanOptions(ctypes.Structure):
         ("bwd_flush", _i32),
         ("bwd_piece_edges", _i32),
         ("bwd_chunk_bounds", _i32),
+        ("fwd_fixed", _i32),
     ]
 
 

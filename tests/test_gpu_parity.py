@@ -192,6 +192,60 @@ def test_spgemm_forward_duplicate_selectors_summed(gpu):
     assert_close(out, ref, mag)
 
 
+def _fwd_both_paths(gpu, p, ix, v, od, oi, d, k, **opts):
+    n = p.size - 1
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    outs = []
+    for fixed in (1, 2):
+        plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k, options=dict(opts, fwd_fixed=fixed))
+        outs.append(plan.forward(to_dev(od, gpu), to_dev(oi, gpu)).cpu().numpy())
+    return outs
+
+
+@pytest.mark.parametrize("gname", ["synthetic", "community", "empty_rows"])
+@pytest.mark.parametrize("k", [8, 16, 32, 64])
+def test_spgemm_forward_fixed_point_vs_f64_path(gpu, gname, k):
+    """The fixed-point accumulation (fwd_fixed, the default) against the oracle, at the
+    north_star bar and at the bound it guarantees (2^-24 of the f32 result on terms that do
+    not cancel, plus the final f32 rounding); it must really run (its rounding differs from
+    the f64 path's in some last bits)."""
+    p, ix, v = GRAPHS[gname]()
+    d = 256
+    x = graphs.features(p.size - 1, d, seed=k + 5)
+    od, oi = oracle.maxk(x.numpy(), k)
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    fixed, f64 = _fwd_both_paths(gpu, p, ix, v, od, oi, d, k)
+    assert_close(fixed, ref, mag)
+    assert_close(f64, ref, mag)
+    assert oracle.worst_relative(fixed, ref, mag) <= 2.0 ** -24 + 2.0 ** -23
+    if ix.size > 10_000:
+        assert not np.array_equal(fixed, f64)
+
+
+@pytest.mark.parametrize("case", ["wide_range", "inf", "nan", "zeros"])
+def test_spgemm_forward_fixed_point_falls_back(gpu, case):
+    """Inputs the fixed-point bound cannot cover take the f64 path: bitwise the same output
+    as fwd_fixed=2 (a dynamic range of 2^40 in |x|; non-finite values; all zeros)."""
+    p, ix, v = GRAPHS["synthetic"]()
+    n, d, k = p.size - 1, 256, 16
+    x = graphs.features(n, d, seed=3)
+    od, oi = oracle.maxk(x.numpy(), k)
+    od = od.copy()
+    if case == "wide_range":
+        od[::7] *= np.float32(2.0 ** -40)
+    elif case == "inf":
+        od[11, 3] = np.inf
+    elif case == "nan":
+        od[12, 0] = np.nan
+    else:
+        od[:] = 0.0
+    fixed, f64 = _fwd_both_paths(gpu, p, ix, v, od, oi, d, k)
+    assert np.array_equal(fixed.view(np.uint32), f64.view(np.uint32))
+    if case == "wide_range":
+        ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+        assert_close(fixed, ref, mag)
+
+
 # ------------------------------------------------------------------------ SSpMM backward
 @pytest.mark.parametrize("k", [8, 16, 24, 32, 64])
 def test_sspmm_backward_golden(gpu, golden, k):
@@ -453,6 +507,10 @@ PLAN_OPTIONS = [
     dict(quad_loads=1, fwd_chunk3=1), dict(bwd_prefetch=1, bwd_waves=16),
     dict(fwd_two_tables=1), dict(fwd_two_tables=2), dict(fwd_two_tables=1, fwd_prefetch=1),
     dict(fwd_rot_windows=64), dict(fwd_rot_windows=3, fwd_rot_rate=1),
+    # forward accumulation: f64 atomics only; fixed point with the other forward layouts
+    dict(fwd_fixed=2), dict(fwd_fixed=2, fwd_two_tables=1), dict(fwd_fixed=1, fwd_chunk3=1),
+    dict(fwd_fixed=1, fwd_unroll=16), dict(fwd_fixed=1, fwd_tile_rows=64),
+    dict(fwd_fixed=1, quad_loads=1), dict(fwd_fixed=1, fwd_phases=3),
 ]
 
 
@@ -599,7 +657,8 @@ def test_capi_external_workspace_contract(gpu):
     od, oi = oracle.maxk(graphs.features(n, d, seed=61).numpy(), k)
     sd, si = to_dev(od, gpu), to_dev(oi, gpu)
     plan = mk.GraphPlan(dptr, didx, dval, n, idx.numel(), d, k, options={"fwd_two_tables": 2})
-    assert plan.fwd_ws_bytes == n * 128            # one 128-B packed record per node
+    assert plan.fwd_ws_bytes >= n * 128            # one 128-B packed record per node (+ the
+    #                                                fixed-point forward's 256-B stats slot)
     out = torch.empty((n, d), device=gpu)
     P = ctypes.c_void_p
     s = P(torch.cuda.current_stream().cuda_stream)

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--windows", default="0,131072,32768,8192")
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--opts", default="{}")
+    ap.add_argument("--fwd-only", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS["reddit"]
@@ -54,9 +55,10 @@ def main():
         out = torch.empty((n, 256), device=dev)
         gr = torch.empty((n, args.k), device=dev)
         tf = timeit(lambda: plan.forward(sd, si, out))
-        tb = timeit(lambda: plan.backward(g, si, gr))
+        tb = None if args.fwd_only else timeit(lambda: plan.backward(g, si, gr))
         print(json.dumps({"window": w, "table_MB": (w or n) * 128 / 1e6, "fwd_ms": tf,
-                          "bwd_ms": tb, "opts": args.opts}), flush=True)
+                          "bwd_ms": tb, "opts": args.opts,
+                          "lib": os.path.basename(os.environ.get("MAXK_HIP_LIB", "libmaxk_hip.so"))}), flush=True)
         del plan
 
 
