@@ -1,8 +1,10 @@
 """Tool-only probe builds of the product library (never shipped; wrong numerics by design):
-the forward's LDS update swapped, to find what bounds spgemm_fwd_kernel at each k.
-  nolds: no LDS update (a never-true branch keeps the loads and products alive)
-  u64:   ds_add_u64 of the f64 bits (the integer LDS atomic rate)
-  rmw:   plain read-add-write (ds_read_b64 + ds_write_b64, racy)
+one LDS update swapped, to find what bounds a kernel.
+  nolds: forward, no LDS update (a never-true branch keeps the loads and products alive)
+  u64:   forward, ds_add_u64 of the f64 bits (the integer LDS atomic rate)
+  rmw:   forward, plain read-add-write (ds_read_b64 + ds_write_b64, racy)
+  bnolds: backward (sspmm_bwd4, CAS pairs), no compare-and-swap (the reads stay)
+  bu32:   backward, two ds_add_u32 of the float bits per pair instead of the CAS
 Writes tools/libmaxk_probe_<name>.so; select one with MAXK_HIP_LIB=... (maxk_kernels/_lib.py).
   python tools/probe_fwd_build.py [names...]"""
 import os
@@ -22,6 +24,22 @@ BODIES = {
             "        __HIP_MEMORY_SCOPE_WORKGROUP);\n  }\n};"),
     "rmw": "    *p += (double)v;\n  }\n};",
 }
+BWD_ORIG = """          if (ok[u]) {
+            u64 expected = old2[u][h];
+            __hip_atomic_compare_exchange_strong(a + h, &expected,"""
+BWD = {
+    "bnolds": BWD_ORIG.replace("if (ok[u]) {", "if (ok[u] && x[u][2 * h] == 1234.5f) {"),
+    "bu32": """          if (ok[u]) {
+            __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(a + h), __float_as_uint(x[u][2 * h]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(a + h) + 1,
+                                   __float_as_uint(x[u][2 * h + 1]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          if (false) {
+            u64 expected = old2[u][h];
+            __hip_atomic_compare_exchange_strong(a + h, &expected,""",
+}
 SRCS = ["maxk_topk.hip", "spgemm.hip", "plan.hip", "capi.cpp"]
 
 
@@ -32,8 +50,13 @@ def build(name):
         shutil.copytree(os.path.join(PKG, "csrc"), src)
         p = os.path.join(src, "spgemm.hip")
         s = open(p).read()
-        assert s.count(ORIG) == 1, "LdsAcc<MAXK_ACC_F64>::add body changed"
-        open(p, "w").write(s.replace(ORIG, BODIES[name]))
+        if name in BWD:
+            assert s.count(BWD_ORIG) == 1, "sspmm_bwd4 CAS-pair block changed"
+            s = s.replace(BWD_ORIG, BWD[name])
+        else:
+            assert s.count(ORIG) == 1, "LdsAcc<MAXK_ACC_F64>::add body changed"
+            s = s.replace(ORIG, BODIES[name])
+        open(p, "w").write(s)
         objs = []
         for f in SRCS:
             o = os.path.join(tmp, f + ".o")
@@ -50,5 +73,5 @@ def build(name):
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:] or list(BODIES):
+    for n in sys.argv[1:] or list(BODIES) + list(BWD):
         build(n)
