@@ -206,6 +206,8 @@ struct maxk_plan {
   // slots of each column's in-edges (bwd_perm, bwd_colptr)
   int32_t bwd_twopass = 0;
   int32_t bwd_tp_rows = 1;       // R: destination rows per wavefront of the row pass
+  int32_t bwd_tp_csc = 0;        // two-pass: products stored in column order; bwd_perm then
+                                 // holds the inverse map (CSR edge -> column-order slot)
   uint32_t* bwd_erec = nullptr;  // [num_edges][2] CSR order: {column, val}
   float* bwd_tbuf = nullptr;     // [num_edges][k] workspace
   // slab flush of shared blocks (bwd_flush 2): piece 0 of a block stores into grad_sp,

@@ -134,6 +134,13 @@ __global__ __launch_bounds__(256) void fwd_fix_stats_kernel(const FwdTask* __res
   }
 }
 
+__global__ void invert_perm_kernel(const int32_t* __restrict__ perm, int64_t E,
+                                   int32_t* __restrict__ inv) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < E;
+       j += (int64_t)gridDim.x * blockDim.x)
+    inv[perm[j]] = (int32_t)j;
+}
+
 // Sort key of each edge for the backward: its source-column block c / C (a stable radix
 // sort then yields the block-major, destination-row-sorted edge list). Also validates the
 // column ids: any idx outside [0, NC) sets *bad (the compute kernels index the CBSR tables
@@ -329,6 +336,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                  "maxk_plan_create: unknown accumulator kind");
   MAXK_CHECK_ARG(o.fwd_fixed >= 0 && o.fwd_fixed <= 2,
                  "maxk_plan_create: fwd_fixed must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.bwd_tp_store >= 0 && o.bwd_tp_store <= 2,
+                 "maxk_plan_create: bwd_tp_store must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_lds_bytes >= 0 && o.bwd_lds_bytes <= 160 * 1024 &&
                      o.bwd_tasks_per_cu >= 0 && o.fwd_task_cap >= 0 && o.fwd_phases >= 0 &&
                      o.bwd_min_task_edges >= 0 &&
@@ -800,6 +809,13 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       p->device_bytes += (int64_t)E * 12;  // erec + bwd_perm
       hipLaunchKernelGGL(build_erec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx,
                          row_of, R, val, E, p->bwd_erec);
+      p->bwd_tp_csc = o.bwd_tp_store == 2;
+      if (p->bwd_tp_csc) {  // bwd_perm becomes CSR edge -> column-order slot
+        hipLaunchKernelGGL(invert_perm_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
+                           p->bwd_perm, E, ids_in);
+        PLAN_TRY(hipMemcpyAsync(p->bwd_perm, ids_in, sizeof(int32_t) * E,
+                                hipMemcpyDeviceToDevice, s));
+      }
     } else {
       PLAN_TRY(hipMalloc(&p->bwd_row, sizeof(int32_t) * E));
       PLAN_TRY(hipMalloc(&p->bwd_col, sizeof(int32_t) * E));

@@ -1072,11 +1072,14 @@ __global__ __launch_bounds__(256) void sspmm_bwd_csc_kernel(
 // left on the texture path are the k selector bytes per edge; grad_out is read once.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int U, int R>
+// CS (plan->bwd_tp_csc): each edge's k products go to its column-order slot pos[e] of the
+// workspace (full 128-B lines at k = 32), so the column pass streams its slots contiguously
+// instead of gathering them through bwd_perm.
+template <int U, int R, bool CS = false>
 __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
     const int32_t* __restrict__ ptr, const uint32_t* __restrict__ erec,
     const float* __restrict__ G, const uint8_t* __restrict__ sp_index, float* __restrict__ T,
-    int N, int D, int k) {
+    int N, int D, int k, const int32_t* __restrict__ pos) {
   // R rows of kMaxDim floats per wavefront (any u8 selector stays inside the wave's rows)
   __shared__ float grow[256 / kWave][R * kMaxDim];
   const int lane = threadIdx.x & (kWave - 1);
@@ -1131,11 +1134,27 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u)
       sw[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)(c[u] & kFwdColMask) * k + 4 * q);
+    int32_t ps[U];
+    if constexpr (CS) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) ps[u] = pos[min(base + u * EPS + slot, e1 - 1)];
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = base + u * EPS + slot;
-      const uint32_t off = e < e1 ? ((uint32_t)(e - e0) * (uint32_t)k + 4u * q) * 4u : 0xfffffff0u;
       const float* rw = row + (R > 1 ? (c[u] >> kFwdColBits) * kMaxDim : 0);
+      if constexpr (CS) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        f4v o;
+        o.x = v[u] * rw[sw[u] & 0xffu];
+        o.y = v[u] * rw[(sw[u] >> 8) & 0xffu];
+        o.z = v[u] * rw[(sw[u] >> 16) & 0xffu];
+        o.w = v[u] * rw[sw[u] >> 24];
+        if (e < e1)
+          __builtin_nontemporal_store(o, reinterpret_cast<f4v*>(T + (size_t)ps[u] * k + 4 * q));
+        continue;
+      }
+      const uint32_t off = e < e1 ? ((uint32_t)(e - e0) * (uint32_t)k + 4u * q) * 4u : 0xfffffff0u;
       u32x4 o;
       o.x = __float_as_uint(v[u] * rw[sw[u] & 0xffu]);
       o.y = __float_as_uint(v[u] * rw[(sw[u] >> 8) & 0xffu]);
@@ -1152,7 +1171,7 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
 // in-edges perm[colptr[c] .. colptr[c+1]) (64/L slots per step, float4 per lane), reduces
 // over the slots with shuffles and stores grad_sp[c] (every column written once: no memset,
 // no atomics).
-template <int U>
+template <int U, bool CS = false>
 __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
     const int32_t* __restrict__ colptr, const int32_t* __restrict__ perm,
     const float* __restrict__ T, float* __restrict__ grad_sp, int ncols, int k) {
@@ -1168,7 +1187,10 @@ __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
   for (int base = e0; base < e1; base += EPS * U) {
     int32_t pe[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) pe[u] = perm[min(base + u * EPS + slot, e1 - 1)];
+    for (int u = 0; u < U; ++u) {
+      const int j = min(base + u * EPS + slot, e1 - 1);
+      pe[u] = CS ? j : perm[j];  // CS: the slots are already in column order
+    }
     float4 t[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1502,18 +1524,31 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     // the plan checked k % 4 == 0, k / 4 a power of two <= 64, E > 0, NC > 0
     const int R = plan->bwd_tp_rows;
     const dim3 rgrid((N + 4 * R - 1) / (4 * R));
+    const bool cs = plan->bwd_tp_csc;
 #define ROWS_LAUNCH(RR)                                                                   \
-    hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR>), rgrid, dim3(256), 0, s, ptr,       \
-                       plan->bwd_erec, grad_out, sp_index, tbuf_ws, N, D, k)
+    do {                                                                                  \
+      if (cs)                                                                             \
+        hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR, true>), rgrid, dim3(256), 0, s,  \
+                           ptr, plan->bwd_erec, grad_out, sp_index, tbuf_ws, N, D, k,     \
+                           plan->bwd_perm);                                               \
+      else                                                                                \
+        hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR>), rgrid, dim3(256), 0, s, ptr,   \
+                           plan->bwd_erec, grad_out, sp_index, tbuf_ws, N, D, k, nullptr); \
+    } while (0)
     if (R >= 8) ROWS_LAUNCH(8);
     else if (R == 4) ROWS_LAUNCH(4);
     else if (R == 2) ROWS_LAUNCH(2);
     else ROWS_LAUNCH(1);
 #undef ROWS_LAUNCH
     MAXK_LAUNCH_CHECK("sspmm_bwd_rows launch");
-    hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4>), dim3((plan->num_cols + 3) / 4), dim3(256), 0,
-                       s, plan->bwd_colptr, plan->bwd_perm, tbuf_ws, grad_sp,
-                       plan->num_cols, k);
+    if (cs)
+      hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4, true>), dim3((plan->num_cols + 3) / 4),
+                         dim3(256), 0, s, plan->bwd_colptr, nullptr, tbuf_ws, grad_sp,
+                         plan->num_cols, k);
+    else
+      hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4>), dim3((plan->num_cols + 3) / 4), dim3(256),
+                         0, s, plan->bwd_colptr, plan->bwd_perm, tbuf_ws, grad_sp,
+                         plan->num_cols, k);
     MAXK_LAUNCH_CHECK("sspmm_bwd_cols launch");
     return MAXK_OK;
   }

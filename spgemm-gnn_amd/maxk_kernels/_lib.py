@@ -91,6 +91,7 @@ class PlanOptions(ctypes.Structure):
         ("bwd_piece_edges", _i32),
         ("bwd_chunk_bounds", _i32),
         ("fwd_fixed", _i32),
+        ("bwd_tp_store", _i32),
     ]
 
 

@@ -511,6 +511,8 @@ PLAN_OPTIONS = [
     dict(fwd_fixed=2), dict(fwd_fixed=2, fwd_two_tables=1), dict(fwd_fixed=1, fwd_chunk3=1),
     dict(fwd_fixed=1, fwd_unroll=16), dict(fwd_fixed=1, fwd_tile_rows=64),
     dict(fwd_fixed=1, quad_loads=1), dict(fwd_fixed=1, fwd_phases=3),
+    # two-pass backward with the products stored in column order
+    dict(bwd_algo=3, bwd_tp_store=2), dict(bwd_algo=3, bwd_tp_store=1),
 ]
 
 
