@@ -222,6 +222,24 @@ def test_spgemm_forward_fixed_point_vs_f64_path(gpu, gname, k):
         assert not np.array_equal(fixed, f64)
 
 
+@pytest.mark.parametrize("scale", [2.0 ** 24, 2.0 ** -24])
+def test_spgemm_forward_fixed_point_follows_value_refresh(gpu, scale):
+    """The per-task fixed-point bounds are plan state: refresh_values must recompute them (a
+    stale 2^49 budget with values 2^24 times larger would overflow the integer sums; 2^24
+    times smaller would lose 24 bits)."""
+    p, ix, v = GRAPHS["synthetic"]()
+    n, d, k = p.size - 1, 256, 16
+    od, oi = oracle.maxk(graphs.features(n, d, seed=9).numpy(), k)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k, options={"fwd_fixed": 1})
+    v2 = (v * np.float32(scale)).astype(np.float32)
+    plan.refresh_values(to_dev(v2, gpu))
+    out = plan.forward(to_dev(od, gpu), to_dev(oi, gpu))
+    ref, mag = oracle.spgemm_forward(p, ix, v2, od, oi, d, with_mag=True)
+    assert_close(out, ref, mag)
+    assert oracle.worst_relative(out.cpu().numpy(), ref, mag) <= 2.0 ** -24 + 2.0 ** -23
+
+
 @pytest.mark.parametrize("case", ["wide_range", "inf", "nan", "zeros"])
 def test_spgemm_forward_fixed_point_falls_back(gpu, case):
     """Inputs the fixed-point bound cannot cover take the f64 path: bitwise the same output
