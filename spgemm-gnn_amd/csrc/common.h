@@ -156,6 +156,7 @@ struct maxk_plan {
   // {max |x|, min |x|} words live at fwd_xstat_off of the forward workspace
   int32_t fwd_fixed = 0;
   int2* fwd_fix = nullptr;
+  int32_t* fwd_rowptr = nullptr;  // plan copy of ptr for the bounds' row sums
   int64_t fwd_xstat_off = 0;
   maxk::FwdTask* fwd_tasks = nullptr;   // e0/e1 index the permuted edge order below
   int32_t fwd_phases = 1;        // column phases per forward call

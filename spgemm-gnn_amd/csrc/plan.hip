@@ -94,44 +94,74 @@ __global__ void gather_fwd_kernel(const int32_t* __restrict__ perm,
   }
 }
 
-// Fixed-point forward bounds per task (spgemm.hip, fwd_fix_scale): one work-group per task
-// over its edge words. sexp: every row of the task has sum |val| <= 2^sexp over the task's
-// edges (f32 sums, with 2^-10 of headroom for their rounding); gexp = sexp - vexp with every
+// Fixed-point forward bounds per task (spgemm.hip, fwd_fix_scale), from the CSR values in a
+// fixed reduction order (so every plan of the same graph gets the same bounds and the
+// integer sums make the forward bitwise reproducible). fwd_row_sums_kernel: one wavefront
+// per row, rs[r] = {sum |val|, min nonzero |val|, 1 if a value is not finite}.
+__global__ __launch_bounds__(256) void fwd_row_sums_kernel(const int32_t* __restrict__ ptr,
+                                                           const float* __restrict__ val, int N,
+                                                           float4* __restrict__ rs) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int r = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
+  if (r >= N) return;
+  float sum = 0.f, mn = 3.0e38f, bad = 0.f;
+  for (int e = ptr[r] + lane; e < ptr[r + 1]; e += kWave) {
+    const float a = fabsf(val ? val[e] : 1.0f);
+    if (!(a <= 3.0e38f)) bad = 1.f;
+    sum += a;
+    if (a > 0.f) mn = fminf(mn, a);
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    sum += __shfl_xor(sum, o);
+    mn = fminf(mn, __shfl_xor(mn, o));
+    bad = fmaxf(bad, __shfl_xor(bad, o));
+  }
+  if (lane == 0) rs[r] = make_float4(sum, mn, bad, 0.f);
+}
+
+// Per task: sexp with every row's sum |val| <= 2^sexp (2^-10 of headroom for the f32 sums;
+// a split task takes its whole row's sum, an upper bound), gexp = sexp - vexp with every
 // nonzero |val| >= 2^vexp. Non-finite values force the f64 path (gexp = 1000).
-__global__ __launch_bounds__(256) void fwd_fix_stats_kernel(const FwdTask* __restrict__ tasks,
-                                                            const uint2* __restrict__ cv,
-                                                            int2* __restrict__ out) {
-  __shared__ float rsum[kFwdMaxTileRows];
-  __shared__ uint32_t vmin_bits, bad;
-  const FwdTask t = tasks[blockIdx.x];
-  for (int i = threadIdx.x; i < kFwdMaxTileRows; i += blockDim.x) rsum[i] = 0.f;
-  if (threadIdx.x == 0) { vmin_bits = 0x7fffffffu; bad = 0u; }
-  __syncthreads();
-  uint32_t mn = 0x7fffffffu;
-  for (int e = t.e0 + (int)threadIdx.x; e < t.e1; e += blockDim.x) {
-    const uint2 w = cv[e];
-    const uint32_t b = w.y & 0x7fffffffu;
-    if (b >= 0x7f800000u) bad = 1u;
-    if (b) mn = min(mn, b);
-    atomicAdd(&rsum[w.x >> kFwdColBits], __uint_as_float(b));
+__global__ void fwd_fix_stats_kernel(const FwdTask* __restrict__ tasks, int ntasks,
+                                     const float4* __restrict__ rs, int2* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntasks) return;
+  const FwdTask task = tasks[t];
+  const int nr = task.nrows < 0 ? 1 : task.nrows;
+  float smax = 0.f, vmin = 3.0e38f;
+  bool bad = false;
+  for (int i = 0; i < nr; ++i) {
+    const float4 q = rs[task.row0 + i];
+    smax = fmaxf(smax, q.x);
+    vmin = fminf(vmin, q.y);
+    bad = bad || q.z != 0.f;
   }
-  atomicMin(&vmin_bits, mn);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float smax = 0.f;
-    for (int i = 0; i < kFwdMaxTileRows; ++i) smax = fmaxf(smax, rsum[i]);
-    int2 r = make_int2(0, 0);
-    if (bad || !(smax < 3.0e38f)) {
-      r.y = 1000;
-    } else if (smax > 0.f && vmin_bits != 0x7fffffffu) {
-      int es = 0, ev = 0;
-      (void)frexpf(smax * (1.0f + 0x1p-10f), &es);  // smax * (1 + 2^-10) < 2^es
-      (void)frexpf(__uint_as_float(vmin_bits), &ev);  // vmin >= 2^(ev - 1)
-      r.x = es;
-      r.y = es - (ev - 1);
-    }
-    out[blockIdx.x] = r;
+  int2 r = make_int2(0, 0);
+  if (bad || !(smax < 3.0e38f)) {
+    r.y = 1000;
+  } else if (smax > 0.f && vmin < 3.0e38f) {
+    int es = 0, ev = 0;
+    (void)frexpf(smax * (1.0f + 0x1p-10f), &es);  // smax * (1 + 2^-10) < 2^es
+    (void)frexpf(vmin, &ev);                       // vmin >= 2^(ev - 1)
+    r.x = es;
+    r.y = es - (ev - 1);
   }
+  out[t] = r;
+}
+
+// Row sums, then per-task bounds (plan create and maxk_plan_refresh_values).
+static hipError_t fwd_fix_stats(const maxk_plan* p, const int32_t* ptr, const float* val,
+                                hipStream_t s) {
+  float4* rs = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&rs), sizeof(float4) * std::max(p->num_nodes, 1), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fwd_row_sums_kernel, dim3((p->num_nodes + 3) / 4), dim3(256), 0, s, ptr,
+                     val, p->num_nodes, rs);
+  hipLaunchKernelGGL(fwd_fix_stats_kernel, dim3((p->n_fwd_tasks + 255) / 256), dim3(256), 0, s,
+                     p->fwd_tasks, p->n_fwd_tasks, rs, p->fwd_fix);
+  e = hipGetLastError();
+  const hipError_t f = hipFreeAsync(rs, s);
+  return e != hipSuccess ? e : f;
 }
 
 __global__ void invert_perm_kernel(const int32_t* __restrict__ perm, int64_t E,
@@ -250,6 +280,7 @@ static void free_plan(maxk_plan* p) {
   dfree(p->fwd_perm);
   dfree(p->fwd_cv);
   dfree(p->fwd_fix);
+  dfree(p->fwd_rowptr);
   dfree(p->fwd_phase_off);
   dfree(p->zero_rows);
   dfree(p->bwd_tasks);
@@ -586,9 +617,12 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     if (p->fwd_fixed) {
       PLAN_TRY(hipMalloc(&p->fwd_fix, sizeof(int2) * ftasks.size()));
       p->device_bytes += sizeof(int2) * ftasks.size();
-      hipLaunchKernelGGL(fwd_fix_stats_kernel, dim3((int)ftasks.size()), dim3(256), 0, s,
-                         p->fwd_tasks, p->fwd_cv, p->fwd_fix);
-      PLAN_TRY(hipGetLastError());
+      // a copy of ptr: maxk_plan_refresh_values recomputes the bounds without the caller's
+      PLAN_TRY(hipMalloc(&p->fwd_rowptr, sizeof(int32_t) * ((size_t)N + 1)));
+      PLAN_TRY(hipMemcpyAsync(p->fwd_rowptr, ptr, sizeof(int32_t) * ((size_t)N + 1),
+                              hipMemcpyDeviceToDevice, s));
+      p->device_bytes += sizeof(int32_t) * ((int64_t)N + 1);
+      PLAN_TRY(fwd_fix_stats(p, p->fwd_rowptr, val, s));
     }
     // Column windows. Default: one launch whose tiles start their column-sorted sweep at the
     // window a shared clock points to (fwd_rot_ticks per window, about one tile's duration
@@ -1096,9 +1130,13 @@ extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* st
     hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
                        (hipStream_t)stream, p->fwd_perm, nullptr, nullptr, val, p->num_edges,
                        p->fwd_cv, false);
-  if (p->fwd_fix && p->n_fwd_tasks > 0)
-    hipLaunchKernelGGL(fwd_fix_stats_kernel, dim3(p->n_fwd_tasks), dim3(256), 0,
-                       (hipStream_t)stream, p->fwd_tasks, p->fwd_cv, p->fwd_fix);
+  if (p->fwd_fix && p->n_fwd_tasks > 0) {
+    const hipError_t e = fwd_fix_stats(p, p->fwd_rowptr, val, (hipStream_t)stream);
+    if (e != hipSuccess) {
+      set_error(std::string("maxk_plan_refresh_values: ") + hipGetErrorString(e));
+      return (int)e;
+    }
+  }
   MAXK_LAUNCH_CHECK("maxk_plan_refresh_values launch");
   return MAXK_OK;
 }

@@ -222,6 +222,23 @@ def test_spgemm_forward_fixed_point_vs_f64_path(gpu, gname, k):
         assert not np.array_equal(fixed, f64)
 
 
+def test_spgemm_forward_fixed_point_bitwise_reproducible(gpu):
+    """Integer sums do not depend on the order of the LDS atomics, and the bounds come from
+    fixed-order row sums: every call of every plan of a graph gives the same bits."""
+    p, ix, v = GRAPHS["heavy_split"]()
+    n, d, k = p.size - 1, 256, 32
+    od, oi = oracle.maxk(graphs.features(n, d, seed=12).numpy(), k)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    sd, si = to_dev(od, gpu), to_dev(oi, gpu)
+    outs = []
+    for _ in range(2):
+        plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k, options={"fwd_fixed": 1})
+        for _ in range(2):
+            outs.append(plan.forward(sd, si).cpu().numpy().view(np.uint32))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+
+
 @pytest.mark.parametrize("scale", [2.0 ** 24, 2.0 ** -24])
 def test_spgemm_forward_fixed_point_follows_value_refresh(gpu, scale):
     """The per-task fixed-point bounds are plan state: refresh_values must recompute them (a
