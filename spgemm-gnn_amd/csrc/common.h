@@ -36,6 +36,7 @@ constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k atomics) vs it
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
 constexpr double kFwdSlotEdgeRate = 1.6e8;  // edges/s one forward slot sustains at k = 16
+constexpr double kFwdSlotEdgeRateFixed = 2.6e8;  // the same with the fixed-point update
 // CBSR tables (5k bytes per column) above these sizes get packed one-line forward records
 // even where two tables would otherwise be used (plan.hip: k >= 32 / k < 32)
 constexpr double kFwdPackedTableBytes = 150e6;

@@ -632,12 +632,16 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     p->fwd_persistent = o.fwd_persistent ? 1 : 0;
     p->fwd_rot_ticks = 0;
     if (B <= 1 && o.fwd_rotate != 2 && (k % 4 == 0 || p->fwd_chunk3) && nt > 0) {
-      B = o.fwd_rot_windows > 0 ? std::min(o.fwd_rot_windows, 64) : kFwdRotWindows;
+      // the fixed-point kernel sweeps faster: more windows at large k, a higher slot rate
+      // (tools/fwd_opts_sweep.py, Reddit: k = 16 1.23 -> 1.19 ms with 260 M edges/s per slot,
+      // k = 32 1.81 -> 1.77 with 140 M and 32 windows, k = 64 3.44 -> 3.23 with 64 windows)
+      const int Bd = p->fwd_fixed ? (k >= 64 ? 64 : k >= 32 ? 32 : kFwdRotWindows) : kFwdRotWindows;
+      B = o.fwd_rot_windows > 0 ? std::min(o.fwd_rot_windows, 64) : Bd;
       // one turn of the clock per tile: the measured per-slot rate scales as ~1/k (Reddit:
       // 2.4e8, 1.65e8, 0.9e8 edges/s per slot at k = 8, 16, 32; best sweep rates 300, 150-200,
       // 100 M)
       const double rate = o.fwd_rot_rate > 0 ? o.fwd_rot_rate * 1e6
-                                             : std::min(5e8, std::max(2e7, kFwdSlotEdgeRate * 16.0 / k));
+                                             : std::min(5e8, std::max(2e7, (p->fwd_fixed ? kFwdSlotEdgeRateFixed : kFwdSlotEdgeRate) * 16.0 / k));
       const double tile_edges = (double)E / nt;
       const double tile_ticks = tile_edges / rate * 1e8;  // s_memrealtime: 100 MHz
       p->fwd_rot_ticks = (int)std::max(1.0, tile_ticks / B);
@@ -745,7 +749,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   // (Reddit bwd k = 16 1.76 -> 1.70 ms, k = 32 3.08 -> 2.93, k = 64 5.43 -> 4.86; the forward's
   // 8-B edge words gain nothing: forward only on request)
   p->bwd_quad = o.quad_loads != 2;
-  p->fwd_quad = o.quad_loads == 1;
+  // forward quad-shared edge-word loads: with the fixed-point kernel (k = 16 1.19 -> 1.16 ms,
+  // k = 32 1.81 -> 1.78); measured neutral-to-slower on the f64 kernel
+  p->fwd_quad = o.quad_loads == 1 || (o.quad_loads == 0 && p->fwd_fixed);
   if (p->bwd_cas64) p->bwd_ks = nslots + (o.bwd_acc_pad == 1 ? 4 : 0);
   else p->bwd_ks = nslots + ((packed && o.bwd_acc_pad == 2) ? 0 : 1);
   p->bwd_sel_lds = packed && o.bwd_sel_lds != 2 ? 1 : 0;
