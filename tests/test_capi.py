@@ -103,6 +103,41 @@ def test_warp4_file_roundtrip(tmp_path):
     assert np.array_equal(warp4.read_warp4(p), t)
 
 
+def test_warp4_replay_validates_against_ptr(tmp_path):
+    """A reference-generated .warp4 (here: the oracle's chunk rule, the reference's
+    generate_meta.py being absent) replays against ptr; a stale or corrupt one is refused."""
+    ptr, _ = graphs.synthetic_csr(300, 9000, seed=5)
+    hp = ptr.numpy()
+    t = oracle.warp4(hp)
+    warp4.write_warp4(warp4.warp4_path("graph", str(tmp_path)), t)
+    got = warp4.replay_warp4(ptr, "graph", str(tmp_path), strict=True)
+    assert np.array_equal(got, t)
+    assert np.array_equal(warp4.ptr_from_warp4(t, hp.size - 1), hp)
+    # any other exact tiling (shuffled entries, 32-nz chunks) sums the same nonzeros
+    warp4.validate_warp4(t[np.random.default_rng(0).permutation(len(t))], ptr)
+    t32 = oracle.warp4(hp, max_nz=32)
+    warp4.validate_warp4(t32, ptr)
+    with pytest.raises(ValueError, match="canonical"):
+        warp4.validate_warp4(t32, ptr, strict=True)
+    # the graph with one more edge in row 7: the table no longer matches
+    other = hp.copy()
+    other[8:] += 1
+    with pytest.raises(ValueError, match="does not match ptr"):
+        warp4.validate_warp4(t, other)
+    bad = t.copy(); bad[3, 3] = 1
+    with pytest.raises(ValueError, match="4th word"):
+        warp4.validate_warp4(bad, ptr)
+    bad = t.copy(); bad[5, 1] += 1
+    with pytest.raises(ValueError, match="gap or overlap|first chunk"):
+        warp4.validate_warp4(bad, ptr)
+    bad = t.copy(); bad[2, 2] = 65
+    with pytest.raises(ValueError, match="length"):
+        warp4.validate_warp4(bad, ptr)
+    with pytest.raises(ValueError, match="row out of range"):
+        warp4.ptr_from_warp4(t, 10)
+    assert np.array_equal(warp4.ptr_from_warp4(np.zeros((0, 4), np.int32), 3), [0, 0, 0, 0])
+
+
 def test_python_checks_mirror_reference_messages():
     import torch
     x = torch.zeros(4, 8)
