@@ -297,6 +297,30 @@ def main():
     bwd_ms = event_time_ms(bwd, reps)
     fwd_pct = launch_percentiles_ms(fwd, reps)
     bwd_pct = launch_percentiles_ms(bwd, reps)
+    exchange = None
+    if world > 1:
+        # the two exchange steps alone (blocking collectives: torch's current stream waits on
+        # the RCCL stream, so the events bracket them), max over ranks; bytes per rank
+        def all_gather():
+            shard.gather(sp_data, sp_index)
+
+        def reduce_scatter():
+            dist.reduce_scatter_tensor(shard.grad_local,
+                                       grad_sp, op=dist.ReduceOp.SUM)
+
+        dist.barrier()
+        ag_ms = event_time_ms(all_gather, reps)
+        dist.barrier()
+        rs_ms = event_time_ms(reduce_scatter, reps)
+        tx = torch.tensor([ag_ms, rs_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tx, op=dist.ReduceOp.MAX)
+        ag_ms, rs_ms = (float(v) for v in tx.tolist())
+        ag_bytes = 5 * k * part.padded_rows            # received table incl. own slice
+        rs_bytes = 4 * k * part.padded_rows            # grad_sp reduced over all columns
+        exchange = {"all_gather_ms": ag_ms, "reduce_scatter_ms": rs_ms,
+                    "all_gather_bytes": ag_bytes, "reduce_scatter_bytes": rs_bytes,
+                    "all_gather_GBps": ag_bytes / (ag_ms * 1e-3) / 1e9,
+                    "reduce_scatter_GBps": rs_bytes / (rs_ms * 1e-3) / 1e9}
     # the MaxK producer of the path (exact top-k -> CBSR), this rank's rows
     topk_ms = event_time_ms(lambda: mk.maxk_forward(h, k, return_index=True), reps)
     e_loc = info["num_edges"]
@@ -352,6 +376,7 @@ def main():
         },
         "fwd_ms": fwd_ms,
         "bwd_ms": bwd_ms,
+        "exchange": exchange,
         "topk_ms": topk_ms,
         "topk_GBps": (h.numel() * 4 + 5 * h.shape[0] * k) / (topk_ms * 1e-3) / 1e9,
         "fwd_launch_ms": fwd_pct,
