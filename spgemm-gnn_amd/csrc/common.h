@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "maxk_hip.h"
 
@@ -48,6 +49,15 @@ constexpr double kFwdPackedTableBytes16 = 32e6;
 // 1.70 / 5.35; ogbn-proteins k = 8 (15) 0.94 / 2.68
 constexpr double kBwdTwoPassReuse = 0.75;
 constexpr int kBwdRowsPerWave = 4;  // row pass: most destination rows one wavefront stages
+// two-pass backward: the E x k product workspace is cut into row chunks of at most this many
+// bytes (one row pass + one column pass per chunk; bwd_tp_chunks overrides)
+constexpr double kBwdTwoPassWorkspaceCap = 4.0 * (1ull << 30);
+// cost-balanced backward chunks: a (column block, destination row) pair costs this many
+// quarter-edges on top of its edges (its grad_out lines are fetched once per pair). Measured
+// on the Reddit-size 41-community graph in ID order (ascending rows), k = 16: 1, 4, 8, 16, 24
+// quarter-edges ran 2.13, 2.03, 1.95, 2.07, 2.30 ms (equal edges 2.19); uniform graphs are
+// within +-0.3 % of equal edges at every value
+constexpr int kBwdRowCost4 = 8;
 constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (plan: 2 at k >= 32 with
                                      // few edges per block row)
 // Records past the end of the backward edge list that a wave may read (and ignore).
@@ -211,7 +221,20 @@ struct maxk_plan {
   int32_t bwd_tp_csc = 0;        // two-pass: products stored in column order; bwd_perm then
                                  // holds the inverse map (CSR edge -> column-order slot)
   uint32_t* bwd_erec = nullptr;  // [num_edges][2] CSR order: {column, val}
-  float* bwd_tbuf = nullptr;     // [num_edges][k] workspace
+  float* bwd_tbuf = nullptr;     // [max chunk edges][k] workspace
+  // row chunks of the two-pass backward (workspace bounded by kBwdTwoPassWorkspaceCap):
+  // chunk p covers destination rows [tp_rows[p], tp_rows[p+1]) = CSR edges [tp_edges[p],
+  // tp_edges[p+1]); bwd_colptr2[p * NC + c] = first column-sorted position of column c whose
+  // row is >= tp_rows[p] (rows ascend within a column), p = 0 .. P (P = 1: bwd_colptr)
+  int32_t bwd_tp_chunks = 1;
+  std::vector<int32_t> tp_rows;
+  std::vector<int64_t> tp_edges;
+  int32_t* bwd_colptr2 = nullptr;
+  // column order of the packed backward (maxk_plan_options.col_order): bwd_corder[p] = the
+  // source column placed at position p of the column blocks (nullptr: identity). Blocks are
+  // contiguous position ranges, so the order decides which columns share an LDS block.
+  int32_t col_order = 0;
+  int32_t* bwd_corder = nullptr;
   // slab flush of shared blocks (bwd_flush 2): piece 0 of a block stores into grad_sp,
   // piece p > 0 into its [C][k] slab region (bwd_slab_floats f32 in all, at byte
   // bwd_slab_off of the backward workspace, behind the selector words); bwd_combine_kernel
@@ -230,4 +253,6 @@ struct maxk_plan {
   int32_t external_ws = 0;
   int64_t fwd_ws_bytes = 0;
   int64_t bwd_ws_bytes = 0;
+  int32_t bwd_chunk_mode = 3;    // chunk bounds in use: 1 shared rows, 2 equal edges, 3 cost
+  int32_t bwd_row_order = 1;     // rows in the block streams: 1 ascending, 2 scattered
 };

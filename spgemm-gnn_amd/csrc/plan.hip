@@ -19,6 +19,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
+#include <cstddef>
+#include <cstring>
 #include <vector>
 
 #include "common.h"
@@ -177,15 +180,65 @@ __global__ void invert_perm_kernel(const int32_t* __restrict__ perm, int64_t E,
 // with idx and must never read outside them).
 __global__ void bwd_key_kernel(const int32_t* __restrict__ idx, int64_t E, int C, int NC,
                                uint32_t* __restrict__ keys, int32_t* __restrict__ ids,
-                               int* __restrict__ bad) {
+                               int* __restrict__ bad, const int32_t* __restrict__ colpos) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int c = idx[e];
     if (c < 0 || c >= NC) atomicOr(bad, 1);
     const int cc = c < 0 ? 0 : (c >= NC ? NC - 1 : c);
-    keys[e] = (uint32_t)(cc / C);
+    keys[e] = (uint32_t)((colpos ? colpos[cc] : cc) / C);  // block of the column's position
     ids[e] = (int32_t)e;
   }
+}
+
+// The same with the destination row's position in the block stream as the low key bits:
+// key = block << rbits | (ra * row + rb) mod N (bwd_row_order 2, a bijection of the rows:
+// gcd(ra, N) = 1), so a stable sort gives block-major streams whose (block, row) runs come in
+// scattered row order (the edges of a run stay together, in CSR order).
+__global__ void bwd_key64_kernel(const int32_t* __restrict__ idx, const int32_t* __restrict__ row_of,
+                                 int64_t E, int C, int NC, uint64_t* __restrict__ keys,
+                                 int32_t* __restrict__ ids, int* __restrict__ bad,
+                                 const int32_t* __restrict__ colpos, int64_t ra, int64_t rb, int N,
+                                 int rbits) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = idx[e];
+    if (c < 0 || c >= NC) atomicOr(bad, 1);
+    const int cc = c < 0 ? 0 : (c >= NC ? NC - 1 : c);
+    const uint64_t blk = (uint64_t)((colpos ? colpos[cc] : cc) / C);
+    const uint64_t rp = (uint64_t)((ra * (int64_t)row_of[e] + rb) % N);
+    keys[e] = (blk << rbits) | rp;
+    ids[e] = (int32_t)e;
+  }
+}
+
+// Dense runs of the ascending-row block streams: window w = sorted edges [w Wn, (w+1) Wn) is
+// dense when it holds fewer than Wn / 16 (block, row) runs, i.e. > 16 edges per run on average
+// (consecutive rows each with many edges into one block).
+__global__ void dense_window_kernel(const uint32_t* __restrict__ bkey, const int32_t* __restrict__ perm,
+                                    const int32_t* __restrict__ row_of, int64_t E, int Wn,
+                                    int* __restrict__ ndense) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e0 = w * Wn;
+  if (e0 + Wn > E) return;
+  int runs = 1;
+  int32_t pr = row_of[perm[e0]];
+  uint32_t pk = bkey[e0];
+  for (int64_t e = e0 + 1; e < e0 + Wn; ++e) {
+    const int32_t r = row_of[perm[e]];
+    const uint32_t kk = bkey[e];
+    runs += (r != pr || kk != pk) ? 1 : 0;
+    pr = r;
+    pk = kk;
+  }
+  if (runs * 16 < Wn) atomicAdd(ndense, 1);
+}
+
+__global__ void key_block_kernel(const uint64_t* __restrict__ k64, int64_t E, int rbits,
+                                 uint32_t* __restrict__ blk) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x)
+    blk[e] = (uint32_t)(k64[e] >> rbits);
 }
 
 __global__ void gather_bwd_kernel(const int32_t* __restrict__ perm,
@@ -193,12 +246,12 @@ __global__ void gather_bwd_kernel(const int32_t* __restrict__ perm,
                                   const int32_t* __restrict__ idx,
                                   const float* __restrict__ val, int64_t E,
                                   int32_t* __restrict__ brow, int32_t* __restrict__ bcol,
-                                  float* __restrict__ bval) {
+                                  float* __restrict__ bval, const int32_t* __restrict__ colpos) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < E;
        j += (int64_t)gridDim.x * blockDim.x) {
     const int32_t e = perm[j];
     if (brow) brow[j] = row_of[e];
-    if (bcol) bcol[j] = idx[e];
+    if (bcol) bcol[j] = colpos ? colpos[idx[e]] : idx[e];  // the column's block position
     bval[j] = val ? val[e] : 1.0f;
   }
 }
@@ -266,6 +319,185 @@ __global__ void build_erec_kernel(const int32_t* __restrict__ idx,
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Cost-balanced backward chunks (bwd_chunk_bounds 3). An edge costs 4 quarter-units; the first
+// edge of every (column block, destination row) run costs rc4 more: the block's gathers fetch
+// that row's grad_out lines once per pair, so a task's time follows its edges plus its pairs
+// (a row with 110 edges into a block - an ID-ordered community - costs about as much as 4
+// rows with one edge each). cost[e] is written in place and prefix-summed (hipcub).
+__global__ void bwd_cost_kernel(const uint32_t* __restrict__ bkey, const int32_t* __restrict__ row,
+                                int64_t E, int rc4, int64_t* __restrict__ cost) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const bool first = e == 0 || bkey[e] != bkey[e - 1] || row[e] != row[e - 1];
+    cost[e] = 4 + (first ? rc4 : 0);
+  }
+}
+
+__global__ void gather_i32_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ at,
+                                  int n, int32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[at[i]];
+}
+
+// out[i] = first e in [lo[i], hi[i]) with cum[e] > target[i] (hi[i] if none); cum ascends.
+__global__ void upper_bound_kernel(const int64_t* __restrict__ cum, const int64_t* __restrict__ target,
+                                   const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+                                   int n, int32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t a = lo[i], b = hi[i];
+  const int64_t t = target[i];
+  while (a < b) {
+    const int64_t m = (a + b) >> 1;
+    if (cum[m] > t) b = m; else a = m + 1;
+  }
+  out[i] = (int32_t)a;
+}
+
+// cum[offs[b] - 1] (0 for offs[b] == 0): the cost of all blocks before b.
+__global__ void block_cost_kernel(const int64_t* __restrict__ cum, const int32_t* __restrict__ offs,
+                                  int nb, int64_t* __restrict__ out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nb) return;
+  out[b] = offs[b] > 0 ? cum[offs[b] - 1] : 0;
+}
+
+// Two-pass row chunks: out[p * NC + c] = first column-sorted position of column c whose row
+// is >= rows[p] (positions [colptr[c], colptr[c+1]) hold CSR edges perm[.] in row order).
+__global__ void tp_colptr_kernel(const int32_t* __restrict__ colptr, const int32_t* __restrict__ perm,
+                                 const int32_t* __restrict__ row_of, int NC,
+                                 const int32_t* __restrict__ rows, int P, int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)(P + 1) * NC) return;
+  const int p = (int)(i / NC), c = (int)(i - (int64_t)p * NC);
+  int a = colptr[c], b = colptr[c + 1];
+  if (p == P) { out[i] = b; return; }
+  const int32_t r = rows[p];
+  while (a < b) {
+    const int m = (a + b) >> 1;
+    if (row_of[perm[m]] < r) a = m + 1; else b = m;
+  }
+  out[i] = a;
+}
+
+// ---------------------------------------------------------------------------------------
+// Column orders of the backward blocks (maxk_plan_options.col_order).
+//
+// Scattered (2): p -> column (a p + b) mod NC with gcd(a, NC) = 1, a ~ 0.618 NC: every
+// contiguous range of positions (a block) takes columns spread evenly over the ID range, so a
+// community of consecutive IDs is shared by all blocks instead of filling a few of its own.
+__global__ void affine_order_kernel(int NC, int64_t a, int64_t b, int32_t* __restrict__ order) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= NC) return;
+  order[p] = (int32_t)((a * (int64_t)p + b) % NC);
+}
+
+__global__ void invert_order_kernel(const int32_t* __restrict__ order, int NC,
+                                    int32_t* __restrict__ pos) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < NC) pos[order[p]] = p;
+}
+
+// Clustered (3): a spectral embedding of the columns by subspace iteration on M^T M, M the
+// row-normalised adjacency: X <- centre(normalise(M^T (M X))), kEmbedDims random +-1 starting
+// vectors, kEmbedIters rounds. After a few rounds X lies in the span of the leading
+// eigenvectors, where columns that appear in the same rows (a community) sit close together;
+// a Morton sort of the quantised coordinates then puts them at neighbouring positions, i.e.
+// in the same blocks. On graphs without such structure the order is as good as random.
+constexpr int kEmbedDims = 8;
+constexpr int kEmbedIters = 3;
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+
+__global__ void embed_init_kernel(int NC, float* __restrict__ X) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)NC * kEmbedDims) return;
+  X[i] = (mix32((uint32_t)i * 2654435761u + 97u) & 1u) ? 1.f : -1.f;
+}
+
+// out[r] = mean over the edges (r, c) of in[c] (one wavefront per row; lanes stride over the
+// row's edges, each holding kEmbedDims partial sums, then a shuffle reduction).
+__global__ __launch_bounds__(256) void embed_spmm_kernel(const int32_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ nbr, int N,
+                                                         const float* __restrict__ in,
+                                                         float* __restrict__ out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int r = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
+  if (r >= N) return;
+  const int e0 = ptr[r], e1 = ptr[r + 1];
+  float a[kEmbedDims];
+#pragma unroll
+  for (int j = 0; j < kEmbedDims; ++j) a[j] = 0.f;
+  for (int e = e0 + lane; e < e1; e += kWave) {
+    const float4* x = reinterpret_cast<const float4*>(in + (size_t)nbr[e] * kEmbedDims);
+    const float4 u = x[0], v = x[1];
+    a[0] += u.x; a[1] += u.y; a[2] += u.z; a[3] += u.w;
+    a[4] += v.x; a[5] += v.y; a[6] += v.z; a[7] += v.w;
+  }
+#pragma unroll
+  for (int j = 0; j < kEmbedDims; ++j)
+    for (int o = kWave / 2; o > 0; o >>= 1) a[j] += __shfl_xor(a[j], o);
+  if (lane < kEmbedDims) {
+    float s = a[0];
+#pragma unroll
+    for (int j = 1; j < kEmbedDims; ++j) s = lane == j ? a[j] : s;
+    out[(size_t)r * kEmbedDims + lane] = e1 > e0 ? s / (float)(e1 - e0) : 0.f;
+  }
+}
+
+// Per-dimension sums and sums of squares (atomics per work-group) for centring/normalising.
+__global__ __launch_bounds__(256) void embed_moments_kernel(const float* __restrict__ X, int NC,
+                                                            float* __restrict__ mom) {
+  __shared__ float sh[2 * kEmbedDims];
+  if (threadIdx.x < 2 * kEmbedDims) sh[threadIdx.x] = 0.f;
+  __syncthreads();
+  const int j = threadIdx.x & (kEmbedDims - 1);
+  float s = 0.f, q = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)NC * kEmbedDims;
+       i += (int64_t)gridDim.x * blockDim.x) {  // blockDim % kEmbedDims == 0: i % 8 == j
+    const float x = X[i];
+    s += x;
+    q += x * x;
+  }
+  atomicAdd(&sh[j], s);
+  atomicAdd(&sh[kEmbedDims + j], q);
+  __syncthreads();
+  if (threadIdx.x < 2 * kEmbedDims) atomicAdd(&mom[threadIdx.x], sh[threadIdx.x]);
+}
+
+__global__ void embed_normalise_kernel(float* __restrict__ X, int NC, const float* __restrict__ mom) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)NC * kEmbedDims) return;
+  const int j = (int)(i & (kEmbedDims - 1));
+  const float mu = mom[j] / NC;
+  const float var = fmaxf(mom[kEmbedDims + j] / NC - mu * mu, 0.f);
+  X[i] = (X[i] - mu) * (var > 0.f ? rsqrtf(var) : 0.f);
+}
+
+// 64-bit Morton key of the 8 coordinates quantised to 8 bits (+-4 standard deviations).
+__global__ void embed_morton_kernel(const float* __restrict__ X, int NC, uint64_t* __restrict__ key,
+                                    int32_t* __restrict__ ids) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= NC) return;
+  uint64_t k = 0;
+  uint32_t q[kEmbedDims];
+#pragma unroll
+  for (int j = 0; j < kEmbedDims; ++j) {
+    const float v = X[(size_t)c * kEmbedDims + j] * 32.f + 128.f;
+    q[j] = (uint32_t)fminf(fmaxf(v, 0.f), 255.f);
+  }
+#pragma unroll
+  for (int b = 7; b >= 0; --b)
+#pragma unroll
+    for (int j = 0; j < kEmbedDims; ++j) k = (k << 1) | ((q[j] >> b) & 1u);
+  key[c] = k;
+  ids[c] = c;
+}
+
 static void dfree(void* q) { if (q) (void)hipFree(q); }
 
 static int grid_for(int64_t n, int threads) {
@@ -294,7 +526,92 @@ static void free_plan(maxk_plan* p) {
   dfree(p->bwd_erec);
   dfree(p->bwd_tbuf);
   dfree(p->bwd_combine);
+  dfree(p->bwd_colptr2);
+  dfree(p->bwd_corder);
   delete p;
+}
+
+// Column order of the backward blocks (col_order 2 scattered, 3 clustered, 4 the caller's):
+// *order = device int32 [NC], order[p] = column at position p. row_of: row of each CSR edge.
+static hipError_t build_col_order(int mode, const int32_t* ptr, const int32_t* idx,
+                                  const int32_t* row_of, int N, int NC, int64_t E,
+                                  const int32_t* user, hipStream_t s, int32_t** order) {
+  hipError_t e = hipMalloc(order, sizeof(int32_t) * (size_t)NC);
+  if (e != hipSuccess) return e;
+  const int g = (NC + 255) / 256;
+  if (mode == 4) return hipMemcpyAsync(*order, user, sizeof(int32_t) * (size_t)NC,
+                                       hipMemcpyDeviceToDevice, s);
+  if (mode == 2 || E == 0) {
+    // a ~ 0.618 NC, coprime with NC (b: a fixed offset)
+    int64_t a = std::max<int64_t>(1, (int64_t)(0.6180339887 * NC));
+    auto gcd = [](int64_t x, int64_t y) { while (y) { const int64_t t = x % y; x = y; y = t; } return x; };
+    while (gcd(a, NC) != 1) ++a;
+    hipLaunchKernelGGL(affine_order_kernel, dim3(g), dim3(256), 0, s, NC, a % NC,
+                       (int64_t)(NC / 3), *order);
+    return hipGetLastError();
+  }
+  // clustered: column CSR (rows sorted by column), subspace iteration, Morton sort
+  uint32_t *kin = nullptr, *kout = nullptr;
+  int32_t *crow = nullptr, *cptr = nullptr, *ids = nullptr;
+  float *X = nullptr, *Y = nullptr, *mom = nullptr;
+  uint64_t *mk = nullptr, *mk2 = nullptr;
+  void* tmp = nullptr;
+  auto cleanup = [&]() {
+    dfree(kin); dfree(kout); dfree(crow); dfree(cptr); dfree(ids); dfree(X); dfree(Y);
+    dfree(mom); dfree(mk); dfree(mk2); dfree(tmp);
+  };
+#define ORD_TRY(x)                      \
+  do {                                  \
+    const hipError_t e_ = (x);          \
+    if (e_ != hipSuccess) {             \
+      cleanup();                        \
+      return e_;                        \
+    }                                   \
+  } while (0)
+  int cbits = 1;
+  while ((1ll << cbits) < (long long)NC) ++cbits;
+  ORD_TRY(hipMalloc(&kin, sizeof(uint32_t) * E));
+  ORD_TRY(hipMalloc(&kout, sizeof(uint32_t) * E));
+  ORD_TRY(hipMalloc(&crow, sizeof(int32_t) * E));
+  ORD_TRY(hipMemcpyAsync(kin, idx, sizeof(int32_t) * E, hipMemcpyDeviceToDevice, s));
+  size_t tb = 0;
+  ORD_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, row_of, crow, (int)E, 0, cbits, s));
+  ORD_TRY(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+  ORD_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, row_of, crow, (int)E, 0, cbits, s));
+  ORD_TRY(hipMalloc(&cptr, sizeof(int32_t) * ((size_t)NC + 1)));
+  hipLaunchKernelGGL(key_offsets_kernel, dim3(NC / 256 + 1), dim3(256), 0, s, kout, E, NC, cptr);
+  ORD_TRY(hipGetLastError());
+  dfree(kin); kin = nullptr;
+  ORD_TRY(hipMalloc(&X, sizeof(float) * kEmbedDims * (size_t)NC));
+  ORD_TRY(hipMalloc(&Y, sizeof(float) * kEmbedDims * (size_t)std::max(N, 1)));
+  ORD_TRY(hipMalloc(&mom, sizeof(float) * 2 * kEmbedDims));
+  const int gx = (int)(((int64_t)NC * kEmbedDims + 255) / 256);
+  hipLaunchKernelGGL(embed_init_kernel, dim3(gx), dim3(256), 0, s, NC, X);
+  for (int it = 0; it < kEmbedIters; ++it) {
+    hipLaunchKernelGGL(embed_spmm_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, idx, N, X, Y);
+    hipLaunchKernelGGL(embed_spmm_kernel, dim3((NC + 3) / 4), dim3(256), 0, s, cptr, crow, NC, Y, X);
+    ORD_TRY(hipMemsetAsync(mom, 0, sizeof(float) * 2 * kEmbedDims, s));
+    hipLaunchKernelGGL(embed_moments_kernel, dim3(std::min(gx, 1024)), dim3(256), 0, s, X, NC, mom);
+    hipLaunchKernelGGL(embed_normalise_kernel, dim3(gx), dim3(256), 0, s, X, NC, mom);
+    ORD_TRY(hipGetLastError());
+  }
+  ORD_TRY(hipMalloc(&mk, sizeof(uint64_t) * NC));
+  ORD_TRY(hipMalloc(&mk2, sizeof(uint64_t) * NC));
+  ORD_TRY(hipMalloc(&ids, sizeof(int32_t) * NC));
+  hipLaunchKernelGGL(embed_morton_kernel, dim3(g), dim3(256), 0, s, X, NC, mk, ids);
+  ORD_TRY(hipGetLastError());
+  size_t tb2 = 0;
+  ORD_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, mk, mk2, ids, *order, NC, 0, 64, s));
+  if (tb2 > tb) {
+    dfree(tmp);
+    tmp = nullptr;
+    ORD_TRY(hipMalloc(&tmp, tb2));
+  }
+  ORD_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb2, mk, mk2, ids, *order, NC, 0, 64, s));
+  ORD_TRY(hipStreamSynchronize(s));
+  cleanup();
+#undef ORD_TRY
+  return hipSuccess;
 }
 
 // Forward task list from a host copy of ptr.
@@ -353,13 +670,46 @@ extern "C" int maxk_plan_create_rect(const int32_t* ptr, const int32_t* idx, con
   return maxk_plan_create_ex(ptr, idx, val, N, NC, E, D, k, nullptr, stream, out_plan);
 }
 
+static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float* val, int32_t N,
+                            int32_t NC, int64_t E, int32_t D, int32_t k,
+                            const maxk_plan_options& o, const int32_t* user_order, void* stream,
+                            maxk_plan** out_plan);
+
 extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const float* val,
                                    int32_t N, int32_t NC, int64_t E, int32_t D, int32_t k,
                                    const maxk_plan_options* opts, void* stream,
                                    maxk_plan** out_plan) {
+  // the version-1 layout: a binding of ABI 1 passes a struct of exactly these bytes
+  return maxk_plan_create_sized(ptr, idx, val, N, NC, E, D, k, opts,
+                                opts ? MAXK_PLAN_OPTIONS_V1_BYTES : 0, nullptr, stream, out_plan);
+}
+
+extern "C" int maxk_plan_create_sized(const int32_t* ptr, const int32_t* idx, const float* val,
+                                      int32_t N, int32_t NC, int64_t E, int32_t D, int32_t k,
+                                      const maxk_plan_options* opts, int64_t opts_bytes,
+                                      const int32_t* col_order, void* stream,
+                                      maxk_plan** out_plan) {
   MAXK_CHECK_ARG(out_plan != nullptr, "maxk_plan_create: out_plan is null");
+  *out_plan = nullptr;
+  MAXK_CHECK_ARG(opts_bytes >= 0 && opts_bytes % 4 == 0 && (opts || opts_bytes == 0),
+                 "maxk_plan_create_sized: opts_bytes must be a multiple of 4 (0 with no opts)");
   maxk_plan_options o{};
-  if (opts) o = *opts;
+  const int64_t mine = (int64_t)sizeof(maxk_plan_options);
+  if (opts) {
+    std::memcpy(&o, opts, (size_t)std::min(opts_bytes, mine));
+    // a newer caller's fields this library does not know must be 0 (their default)
+    const uint8_t* extra = reinterpret_cast<const uint8_t*>(opts);
+    for (int64_t b = mine; b < opts_bytes; ++b)
+      MAXK_CHECK_ARG(extra[b] == 0, "maxk_plan_create_sized: unknown option fields are set "
+                                    "(the caller's maxk_plan_options is newer than this library)");
+  }
+  return plan_create_impl(ptr, idx, val, N, NC, E, D, k, o, col_order, stream, out_plan);
+}
+
+static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float* val, int32_t N,
+                            int32_t NC, int64_t E, int32_t D, int32_t k,
+                            const maxk_plan_options& o, const int32_t* user_order, void* stream,
+                            maxk_plan** out_plan) {
   MAXK_CHECK_ARG(o.fwd_tile_rows >= 0 && o.fwd_tile_rows <= kFwdMaxTileRows,
                  "maxk_plan_create: fwd_tile_rows must be in [0, 32]");
   MAXK_CHECK_ARG(o.fwd_accumulator >= 0 && o.fwd_accumulator <= MAXK_ACC_F32_CAS &&
@@ -432,8 +782,17 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   MAXK_CHECK_ARG(o.bwd_flush >= 0 && o.bwd_flush <= 2,
                  "maxk_plan_create: bwd_flush must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_piece_edges >= 0, "maxk_plan_create: bwd_piece_edges must be >= 0");
-  MAXK_CHECK_ARG(o.bwd_chunk_bounds >= 0 && o.bwd_chunk_bounds <= 2,
-                 "maxk_plan_create: bwd_chunk_bounds must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.bwd_chunk_bounds >= 0 && o.bwd_chunk_bounds <= 3,
+                 "maxk_plan_create: bwd_chunk_bounds must be 0, 1, 2 or 3");
+  MAXK_CHECK_ARG(o.bwd_row_cost >= 0 && o.bwd_row_cost <= 4096,
+                 "maxk_plan_create: bwd_row_cost must be in [0, 4096]");
+  MAXK_CHECK_ARG(o.col_order >= 0 && o.col_order <= 4,
+                 "maxk_plan_create: col_order must be 0 .. 4");
+  MAXK_CHECK_ARG(o.col_order != 4 || user_order != nullptr || NC == 0,
+                 "maxk_plan_create: col_order 4 needs the col_order argument");
+  MAXK_CHECK_ARG(o.bwd_tp_chunks >= 0, "maxk_plan_create: bwd_tp_chunks must be >= 0");
+  MAXK_CHECK_ARG(o.bwd_row_order >= 0 && o.bwd_row_order <= 2,
+                 "maxk_plan_create: bwd_row_order must be 0, 1 or 2");
   maxk_plan* p = new maxk_plan();
   p->external_ws = o.external_workspace;
   p->num_nodes = N;
@@ -499,7 +858,11 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   void* temp = nullptr;
   int64_t* d_offs = nullptr;
   int* d_bad = nullptr;
+  int32_t* order = nullptr;   // column order: position -> column (col_order 2..4)
+  int32_t* colpos = nullptr;  // column -> position
   auto fail = [&](int rc) {
+    dfree(order);
+    dfree(colpos);
     dfree(row_of);
     dfree(keys_in);
     dfree(keys_out);
@@ -533,6 +896,45 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       return fail(MAXK_ERR_INVALID_ARG);
     }
   }
+  // ---------------- column order (col_order 2 scattered, 3 clustered, 4 the caller's): the
+  // backward's packed kernels take their column blocks as position ranges of it. The forward
+  // keeps its column-sorted sweep: sweeping in the clustered order measured much slower
+  // (shuffled 41-community Reddit-size graph: k = 16 1.07 -> 1.36 ms, k = 32 1.61 -> 2.75)
+  const int order_mode = o.col_order == 0 ? 1 : o.col_order;
+  if (order_mode >= 2 && NC > 0) {
+    if (E > 0) {
+      PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
+      hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
+      PLAN_TRY(hipGetLastError());
+    }
+    PLAN_TRY(build_col_order(order_mode, ptr, idx, row_of, N, NC, E, user_order, s, &order));
+    PLAN_TRY(hipMalloc(&colpos, sizeof(int32_t) * NC));
+    PLAN_TRY(hipMemsetAsync(colpos, 0xff, sizeof(int32_t) * NC, s));
+    hipLaunchKernelGGL(invert_order_kernel, dim3((NC + 255) / 256), dim3(256), 0, s, order, NC, colpos);
+    PLAN_TRY(hipGetLastError());
+    if (order_mode == 4) {  // the caller's order must be a permutation of [0, NC)
+      std::vector<int32_t> ho(NC), hc(NC);
+      PLAN_TRY(hipMemcpyAsync(ho.data(), order, sizeof(int32_t) * NC, hipMemcpyDeviceToHost, s));
+      PLAN_TRY(hipStreamSynchronize(s));
+      bool ok = true;
+      for (int i = 0; i < NC && ok; ++i) ok = ho[i] >= 0 && ho[i] < NC;
+      if (ok) {
+        PLAN_TRY(hipMemcpyAsync(hc.data(), colpos, sizeof(int32_t) * NC, hipMemcpyDeviceToHost, s));
+        PLAN_TRY(hipStreamSynchronize(s));
+        for (int i = 0; i < NC && ok; ++i) ok = hc[i] >= 0 && ho[hc[i]] == i;
+      }
+      if (!ok) {
+        set_error("maxk_plan_create: col_order is not a permutation of [0, num_cols)");
+        return fail(MAXK_ERR_INVALID_ARG);
+      }
+    }
+  }
+  auto drop_order = [&]() {
+    dfree(order);
+    dfree(colpos);
+    order = colpos = nullptr;
+  };
+
   std::vector<FwdTask> ftasks;
   std::vector<int32_t> zrows;
   build_fwd_tasks(hp, N, p->fwd_tile_rows, o.fwd_task_cap, ftasks, zrows);
@@ -579,8 +981,10 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       PLAN_TRY(_e2);                          \
     }                                         \
   } while (0)
-      FWD_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
-      hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
+      if (!row_of) {
+        FWD_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
+        hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
+      }
       FWD_TRY(hipMalloc(&d_starts, sizeof(int32_t) * nt));
       FWD_TRY(hipMalloc(&d_ranks, sizeof(int32_t) * nt));
       FWD_TRY(hipMalloc(&d_row0s, sizeof(int32_t) * nt));
@@ -804,6 +1208,24 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   }
   const bool colsort = p->bwd_csc || p->bwd_twopass;
   const bool xcd_order = o.bwd_order == 0 && !colsort;
+  // the column order applies to the packed column-block kernels (their tasks own position
+  // ranges; the column-major kernels sort by the column itself)
+  const int32_t* bcolpos = (colpos && packed && !colsort) ? colpos : nullptr;
+  // row order inside the blocks' streams (column-block kernels; the shared row chunk bounds
+  // need ascending rows): scattered by an affine bijection ra * row + rb mod N
+  const bool row_hash_ok = !colsort && E > 0 && N > 1 && o.bwd_chunk_bounds != 1;
+  bool row_hash = row_hash_ok && o.bwd_row_order == 2;
+  int64_t ra = 1, rb = 0;
+  int rbits = 1;
+  if (row_hash_ok) {
+    auto gcd = [](int64_t x, int64_t y) { while (y) { const int64_t t = x % y; x = y; y = t; } return x; };
+    ra = std::max<int64_t>(1, (int64_t)(0.6180339887 * N));
+    while (gcd(ra, N) != 1) ++ra;
+    ra %= N;
+    rb = N / 7;
+    while ((1ll << rbits) < (long long)N) ++rbits;
+  }
+  auto row_pos = [&](int32_t r) -> int64_t { return row_hash ? (ra * (int64_t)r + rb) % N : r; };
   int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
   if (xcd_order && nblocks >= kXcds) {
     // a multiple of the XCD count, so every XCD owns the same number of column blocks; and
@@ -817,6 +1239,7 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
   p->bwd_block_cols = C;
   p->n_bwd_blocks = nblocks;
   std::vector<int64_t> offs(colsort ? 1 : nblocks + 1, 0);
+  p->bwd_row_order = colsort ? 0 : 1;
   if (E > 0) {
     if (!row_of) {
       PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
@@ -828,20 +1251,117 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
     PLAN_TRY(hipMalloc(&p->bwd_perm, sizeof(int32_t) * E));
     PLAN_TRY(hipMalloc(&d_bad, sizeof(int)));
     PLAN_TRY(hipMemsetAsync(d_bad, 0, sizeof(int), s));
-    hipLaunchKernelGGL(bwd_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, E, C, NC,
-                       keys_in, ids_in, d_bad);
-    PLAN_TRY(hipGetLastError());
     int end_bit = 1;
     while ((1ll << end_bit) < (long long)nblocks) ++end_bit;
-    size_t temp_bytes = 0;
-    PLAN_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, ids_in,
-                                                p->bwd_perm, (int)E, 0, end_bit, s));
-    PLAN_TRY(hipMalloc(&temp, temp_bytes));
-    PLAN_TRY(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, ids_in,
-                                                p->bwd_perm, (int)E, 0, end_bit, s));
+    // the block-major sort: keys_out = block id of each sorted edge, bwd_perm = its CSR id
+    auto sort_blocks = [&](bool hash) -> hipError_t {
+      size_t temp_bytes = 0;
+      dfree(temp);
+      temp = nullptr;
+      if (!hash) {
+        hipLaunchKernelGGL(bwd_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, E, C, NC,
+                           keys_in, ids_in, d_bad, bcolpos);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, ids_in,
+                                               p->bwd_perm, (int)E, 0, end_bit, s);
+        if (e != hipSuccess) return e;
+        e = hipMalloc(&temp, temp_bytes);
+        if (e != hipSuccess) return e;
+        return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, ids_in,
+                                                  p->bwd_perm, (int)E, 0, end_bit, s);
+      }
+      // 64-bit keys {block, row position}; their block ids then go to keys_out
+      uint64_t *k64_in = nullptr, *k64_out = nullptr;
+      const hipError_t ke = [&]() -> hipError_t {
+        hipError_t e = hipMalloc(&k64_in, sizeof(uint64_t) * E);
+        if (e != hipSuccess) return e;
+        e = hipMalloc(&k64_out, sizeof(uint64_t) * E);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(bwd_key64_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, row_of,
+                           E, C, NC, k64_in, ids_in, d_bad, bcolpos, ra, rb, N, rbits);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, k64_in, k64_out, ids_in,
+                                               p->bwd_perm, (int)E, 0, end_bit + rbits, s);
+        if (e != hipSuccess) return e;
+        e = hipMalloc(&temp, temp_bytes);
+        if (e != hipSuccess) return e;
+        e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k64_in, k64_out, ids_in,
+                                               p->bwd_perm, (int)E, 0, end_bit + rbits, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(key_block_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, k64_out, E,
+                           rbits, keys_out);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return hipStreamSynchronize(s);
+      }();
+      dfree(k64_in);
+      dfree(k64_out);
+      return ke;
+    };
+    PLAN_TRY(sort_blocks(row_hash));
+    if (row_hash_ok && o.bwd_row_order == 0) {
+      // auto: scatter the rows when the ascending-row streams are mostly dense runs, i.e. many
+      // consecutive rows with many edges into the same block (an ID-ordered community: Reddit
+      // size, 41 communities, k = 16: 2.31 -> 1.59 ms; k = 32: 3.62 -> 2.45); with rows that
+      // are unrelated to their neighbours the ascending order is 2-3 % faster (uniform
+      // Reddit: 1.686 vs 1.715 ms at k = 16, 2.61 vs 2.69 at k = 32)
+      constexpr int Wn = 2048;
+      const int64_t nw = E / Wn;
+      if (nw > 0) {
+        int* d_nd = nullptr;
+        int nd = 0;
+        const hipError_t de = [&]() -> hipError_t {
+          hipError_t e = hipMalloc(&d_nd, sizeof(int));
+          if (e != hipSuccess) return e;
+          e = hipMemsetAsync(d_nd, 0, sizeof(int), s);
+          if (e != hipSuccess) return e;
+          hipLaunchKernelGGL(dense_window_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s,
+                             keys_out, p->bwd_perm, row_of, E, Wn, d_nd);
+          e = hipGetLastError();
+          if (e != hipSuccess) return e;
+          e = hipMemcpyAsync(&nd, d_nd, sizeof(int), hipMemcpyDeviceToHost, s);
+          if (e != hipSuccess) return e;
+          return hipStreamSynchronize(s);
+        }();
+        dfree(d_nd);
+        PLAN_TRY(de);
+        if (nd > nw / 4) {
+          row_hash = true;
+          PLAN_TRY(sort_blocks(true));
+        }
+      }
+    }
+    if (!colsort) p->bwd_row_order = row_hash ? 2 : 1;
     if (p->bwd_twopass) {
       PLAN_TRY(hipMalloc(&p->bwd_erec, sizeof(uint32_t) * 2 * (size_t)E));
-      p->bwd_ws_bytes = (int64_t)E * k * 4;  // the E x k product workspace
+      p->bwd_tp_csc = o.bwd_tp_store == 2;
+      // row chunks: the workspace holds one chunk's products (column order: one chunk)
+      int P = o.bwd_tp_chunks > 0
+                  ? o.bwd_tp_chunks
+                  : (int)std::max<int64_t>(1, (int64_t)std::ceil((double)E * k * 4.0 /
+                                                                  kBwdTwoPassWorkspaceCap));
+      P = std::max(1, std::min(P, std::max(N, 1)));
+      if (p->bwd_tp_csc) P = 1;
+      p->bwd_tp_chunks = P;
+      p->tp_rows.assign(P + 1, 0);
+      p->tp_edges.assign(P + 1, 0);
+      int64_t max_chunk = 0;
+      for (int q = 1; q <= P; ++q) {
+        int32_t r = N;
+        if (q < P) {
+          // a multiple of R: the row pass's wavefronts stage rows r0 .. r0 + R - 1 with
+          // r0 % R == 0 (the edge records carry row % R)
+          const int64_t target = E * q / P;
+          r = (int32_t)(std::lower_bound(hp.begin(), hp.end(), (int32_t)target) - hp.begin());
+          r = std::max(p->tp_rows[q - 1], std::min(r / R * R, N));
+        }
+        p->tp_rows[q] = r;
+        p->tp_edges[q] = hp[r];
+        max_chunk = std::max<int64_t>(max_chunk, p->tp_edges[q] - p->tp_edges[q - 1]);
+      }
+      p->bwd_ws_bytes = max_chunk * k * 4;  // one row chunk of the E x k product workspace
       if (!p->external_ws) {
         PLAN_TRY(hipMalloc(&p->bwd_tbuf, (size_t)p->bwd_ws_bytes));
         p->device_bytes += p->bwd_ws_bytes;
@@ -849,7 +1369,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       p->device_bytes += (int64_t)E * 12;  // erec + bwd_perm
       hipLaunchKernelGGL(build_erec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx,
                          row_of, R, val, E, p->bwd_erec);
-      p->bwd_tp_csc = o.bwd_tp_store == 2;
       if (p->bwd_tp_csc) {  // bwd_perm becomes CSR edge -> column-order slot
         hipLaunchKernelGGL(invert_perm_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
                            p->bwd_perm, E, ids_in);
@@ -862,7 +1381,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       PLAN_TRY(hipMalloc(&p->bwd_val, sizeof(float) * E));
       p->device_bytes += (int64_t)E * 16;
       hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
-                         p->bwd_perm, row_of, idx, val, E, p->bwd_row, p->bwd_col, p->bwd_val);
+                         p->bwd_perm, row_of, idx, val, E, p->bwd_row, p->bwd_col, p->bwd_val,
+                         bcolpos);
     }
     PLAN_TRY(hipMalloc(&d_offs, sizeof(int32_t) * (nblocks + 1)));
     hipLaunchKernelGGL(key_offsets_kernel, dim3(nblocks / 256 + 1), dim3(256), 0, s, keys_out,
@@ -875,6 +1395,28 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       p->bwd_colptr = reinterpret_cast<int32_t*>(d_offs);
       d_offs = nullptr;
       p->device_bytes += sizeof(int32_t) * (nblocks + 1);
+      if (p->bwd_twopass && p->bwd_tp_chunks > 1) {
+        // per-chunk column pointers (rows ascend within a column of the stable sort)
+        const int P = p->bwd_tp_chunks;
+        int32_t* d_rows = nullptr;
+        PLAN_TRY(hipMalloc(&d_rows, sizeof(int32_t) * (P + 1)));
+        const hipError_t ce = [&]() -> hipError_t {
+          hipError_t e = hipMemcpyAsync(d_rows, p->tp_rows.data(), sizeof(int32_t) * (P + 1),
+                                        hipMemcpyHostToDevice, s);
+          if (e != hipSuccess) return e;
+          e = hipMalloc(&p->bwd_colptr2, sizeof(int32_t) * (size_t)(P + 1) * NC);
+          if (e != hipSuccess) return e;
+          const int64_t n = (int64_t)(P + 1) * NC;
+          hipLaunchKernelGGL(tp_colptr_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                             p->bwd_colptr, p->bwd_perm, row_of, NC, d_rows, P, p->bwd_colptr2);
+          e = hipGetLastError();
+          if (e != hipSuccess) return e;
+          return hipStreamSynchronize(s);
+        }();
+        dfree(d_rows);
+        PLAN_TRY(ce);
+        p->device_bytes += sizeof(int32_t) * (int64_t)(P + 1) * NC;
+      }
       PLAN_TRY(hipStreamSynchronize(s));
     } else {
       std::vector<int32_t> offs32(nblocks + 1);
@@ -931,10 +1473,32 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       nch64 = best;
     }
     const int nch = (int)nch64;
-    std::vector<int32_t> co((size_t)nblocks * (nch + 1));
-    if (o.bwd_chunk_bounds == 1) {
+    // chunk bounds per block: cbd[b] = {offs[b], ..., offs[b+1]} (nch_b + 1 entries)
+    const int mode = o.bwd_chunk_bounds == 0 ? 3 : o.bwd_chunk_bounds;
+    p->bwd_chunk_mode = mode;
+    std::vector<std::vector<int32_t>> cbd((size_t)nblocks);
+    int32_t *d_rb = nullptr, *d_co = nullptr;
+    int64_t *d_cum = nullptr, *d_bc = nullptr, *d_tg = nullptr, *d_lo = nullptr, *d_hi = nullptr;
+    void* d_scan = nullptr;
+    auto chunk_cleanup = [&]() {
+      dfree(d_rb); dfree(d_co); dfree(d_cum); dfree(d_bc); dfree(d_tg); dfree(d_lo); dfree(d_hi);
+      dfree(d_scan);
+      d_rb = d_co = nullptr;
+      d_cum = d_bc = d_tg = d_lo = d_hi = nullptr;
+      d_scan = nullptr;
+    };
+#define CH_TRY(x)                                          \
+    do {                                                   \
+      hipError_t e_ = (x);                                 \
+      if (e_ != hipSuccess) {                              \
+        chunk_cleanup();                                   \
+        PLAN_TRY(e_);                                      \
+      }                                                    \
+    } while (0)
+    if (mode == 1) {
       // shared row bounds: chunk j of every block covers the same rows [R_j, R_j+1) (equal
       // edge counts over the whole graph)
+      std::vector<int32_t> co((size_t)nblocks * (nch + 1));
       std::vector<int32_t> rb(nch + 1);
       for (int j = 0; j <= nch; ++j) {
         const int64_t target = E * j / nch;
@@ -942,16 +1506,6 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       }
       rb[0] = 0;
       rb[nch] = N;
-      int32_t *d_rb = nullptr, *d_co = nullptr;
-      auto chunk_cleanup = [&]() { dfree(d_rb); dfree(d_co); };
-#define CH_TRY(x)                                          \
-      do {                                                 \
-        hipError_t e_ = (x);                               \
-        if (e_ != hipSuccess) {                            \
-          chunk_cleanup();                                 \
-          PLAN_TRY(e_);                                    \
-        }                                                  \
-      } while (0)
       CH_TRY(hipMalloc(&d_rb, sizeof(int32_t) * (nch + 1)));
       CH_TRY(hipMalloc(&d_co, sizeof(int32_t) * co.size()));
       CH_TRY(hipMemcpyAsync(d_rb, rb.data(), sizeof(int32_t) * (nch + 1), hipMemcpyHostToDevice, s));
@@ -961,35 +1515,100 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       CH_TRY(hipGetLastError());
       CH_TRY(hipMemcpyAsync(co.data(), d_co, sizeof(int32_t) * co.size(), hipMemcpyDeviceToHost, s));
       CH_TRY(hipStreamSynchronize(s));
-      chunk_cleanup();
-#undef CH_TRY
-    } else {
+      for (int b = 0; b < nblocks; ++b)
+        cbd[b].assign(co.begin() + (size_t)b * (nch + 1), co.begin() + (size_t)(b + 1) * (nch + 1));
+    } else if (mode == 2) {
       // per-block bounds: chunk j of block b holds edges [j, j+1) * nnz_b / nch of the block's
       // row-sorted stream. On a graph without column locality these are the shared row
       // bounds to within a few rows (the work-groups that run together still sweep the same
       // rows of G); with locality (a community linking mostly into its own blocks) every
       // task keeps an equal share instead of a few tasks carrying most of a chunk
-      // (41-community Reddit-size graph, k = 16: 3.38 -> see DESIGN §6)
+      // (41-community Reddit-size graph, k = 16: 3.38 -> 2.18 ms)
       for (int b = 0; b < nblocks; ++b) {
         const int64_t o0 = offs[b], nnz = offs[b + 1] - offs[b];
-        for (int j = 0; j <= nch; ++j) co[(size_t)b * (nch + 1) + j] = (int32_t)(o0 + nnz * j / nch);
+        cbd[b].resize(nch + 1);
+        for (int j = 0; j <= nch; ++j) cbd[b][j] = (int32_t)(o0 + nnz * j / nch);
+      }
+    } else {
+      // equal cost (bwd_cost_kernel: edges + rc4/4 per (block, row) pair). A task's time
+      // follows the grad_out lines it fetches, once per pair, as much as its edges: with
+      // column locality (an ID-ordered community) a block's stream is a dense run of
+      // community rows (~100 edges per pair) between long sparse stretches (~1 edge per pair),
+      // and equal-edge chunks of it differ several-fold in time. Each block gets chunks in
+      // proportion to its cost (nch on average), each chunk an equal share of that cost.
+      const int rc4 = o.bwd_row_cost ? o.bwd_row_cost : kBwdRowCost4;
+      CH_TRY(hipMalloc(&d_cum, sizeof(int64_t) * E));
+      hipLaunchKernelGGL(bwd_cost_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, keys_out,
+                         p->bwd_row, E, rc4, d_cum);
+      CH_TRY(hipGetLastError());
+      size_t sb = 0;
+      CH_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, sb, d_cum, d_cum, (int)E, s));
+      CH_TRY(hipMalloc(&d_scan, std::max<size_t>(sb, 16)));
+      CH_TRY(hipcub::DeviceScan::InclusiveSum(d_scan, sb, d_cum, d_cum, (int)E, s));
+      CH_TRY(hipMalloc(&d_bc, sizeof(int64_t) * (nblocks + 1)));
+      hipLaunchKernelGGL(block_cost_kernel, dim3(nblocks / 256 + 1), dim3(256), 0, s, d_cum,
+                         reinterpret_cast<const int32_t*>(d_offs), nblocks, d_bc);
+      CH_TRY(hipGetLastError());
+      std::vector<int64_t> bc(nblocks + 1);
+      CH_TRY(hipMemcpyAsync(bc.data(), d_bc, sizeof(int64_t) * (nblocks + 1), hipMemcpyDeviceToHost, s));
+      CH_TRY(hipStreamSynchronize(s));
+      const double tau = std::max(1.0, (double)bc[nblocks] / ((double)nblocks * nch));
+      std::vector<int64_t> tg, lo, hi;
+      std::vector<int32_t> nchb(nblocks);
+      for (int b = 0; b < nblocks; ++b) {
+        const int64_t T = bc[b + 1] - bc[b], nnz = offs[b + 1] - offs[b];
+        int64_t c = std::max<int64_t>(1, std::llround((double)T / tau));
+        c = std::min<int64_t>(c, std::max<int64_t>(1, std::min<int64_t>(nnz, 64ll * nch)));
+        nchb[b] = (int32_t)c;
+        for (int64_t j = 1; j < c; ++j) {
+          tg.push_back(bc[b] + (int64_t)((double)T * j / c));
+          lo.push_back(offs[b]);
+          hi.push_back(offs[b + 1]);
+        }
+      }
+      std::vector<int32_t> cut(tg.size());
+      if (!tg.empty()) {
+        const size_t m = tg.size();
+        CH_TRY(hipMalloc(&d_tg, sizeof(int64_t) * m));
+        CH_TRY(hipMalloc(&d_lo, sizeof(int64_t) * m));
+        CH_TRY(hipMalloc(&d_hi, sizeof(int64_t) * m));
+        CH_TRY(hipMalloc(&d_co, sizeof(int32_t) * m));
+        CH_TRY(hipMemcpyAsync(d_tg, tg.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
+        CH_TRY(hipMemcpyAsync(d_lo, lo.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
+        CH_TRY(hipMemcpyAsync(d_hi, hi.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(upper_bound_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
+                           d_cum, d_tg, d_lo, d_hi, (int)m, d_co);
+        CH_TRY(hipGetLastError());
+        CH_TRY(hipMemcpyAsync(cut.data(), d_co, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s));
+        CH_TRY(hipStreamSynchronize(s));
+      }
+      size_t ci = 0;
+      for (int b = 0; b < nblocks; ++b) {
+        cbd[b].push_back((int32_t)offs[b]);
+        for (int j = 1; j < nchb[b]; ++j) cbd[b].push_back(std::max(cbd[b].back(), cut[ci++]));
+        cbd[b].push_back((int32_t)offs[b + 1]);
       }
     }
+    chunk_cleanup();
+#undef CH_TRY
     // Pieces: a (block, chunk) task holding more than twice the average task's edges is cut
     // into pieces of equal edge counts (work-groups of their own, in the same chunk-major
     // slot). The shared row bounds assume edges spread evenly over the blocks; with column
     // locality (a community of rows linking mostly into its own blocks) a few
-    // tasks would otherwise carry most of a chunk's edges.
+    // tasks would otherwise carry most of a chunk's edges. Cost-balanced chunks need none
+    // (unless bwd_piece_edges asks for them).
     const int64_t avg_task = std::max<int64_t>(1, E / ((int64_t)nblocks * nch));
     const int64_t piece_cap = o.bwd_piece_edges > 0 ? (int64_t)o.bwd_piece_edges
-                                                    : std::max<int64_t>(2 * avg_task, 16384);
+                              : mode == 3 ? (int64_t)INT32_MAX
+                                          : std::max<int64_t>(2 * avg_task, 16384);
     const bool slab_flush = packed && o.bwd_flush != 1;
+    auto npieces = [&](int64_t e) {
+      return (int32_t)std::max<int64_t>(1, (e + piece_cap - 1) / piece_cap);
+    };
     std::vector<int32_t> pieces_of((size_t)nblocks, 0);
-    for (int j = 0; j < nch; ++j)
-      for (int b = 0; b < nblocks; ++b) {
-        const int64_t e = (int64_t)co[(size_t)b * (nch + 1) + j + 1] - co[(size_t)b * (nch + 1) + j];
-        pieces_of[b] += (int32_t)std::max<int64_t>(1, (e + piece_cap - 1) / piece_cap);
-      }
+    for (int b = 0; b < nblocks; ++b)
+      for (size_t j = 0; j + 1 < cbd[b].size(); ++j)
+        pieces_of[b] += npieces((int64_t)cbd[b][j + 1] - cbd[b][j]);
     // compact slab regions: block b's pieces 1 .. P_b - 1 own C x k floats each
     std::vector<int64_t> slab_base((size_t)nblocks, -1);
     std::vector<int4> comb;
@@ -1008,27 +1627,73 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       slab_floats = 0;
       std::fill(slab_base.begin(), slab_base.end(), -1);
     }
+    // Row-major emission: chunks ordered by the first destination row they sweep (then by
+    // block), so the work-groups that run together sweep about the same rows of G and share
+    // its lines in L2. With nch equal-edge chunks per block on a graph without column
+    // locality this is the chunk-major order (chunk j of every block starts near the same
+    // row); with locality it keeps the sparse stretches of different blocks together.
+    std::vector<int32_t> first_row;
+    {
+      std::vector<int32_t> starts;
+      for (int b = 0; b < nblocks; ++b)
+        for (size_t j = 0; j + 1 < cbd[b].size(); ++j)
+          starts.push_back(std::min<int32_t>(cbd[b][j], (int32_t)std::max<int64_t>(E - 1, 0)));
+      first_row.resize(starts.size());
+      int32_t *d_st = nullptr, *d_fr = nullptr;
+      auto fr_cleanup = [&]() { dfree(d_st); dfree(d_fr); };
+      const hipError_t fe = [&]() -> hipError_t {
+        hipError_t e = hipMalloc(&d_st, sizeof(int32_t) * starts.size());
+        if (e != hipSuccess) return e;
+        e = hipMalloc(&d_fr, sizeof(int32_t) * starts.size());
+        if (e != hipSuccess) return e;
+        e = hipMemcpyAsync(d_st, starts.data(), sizeof(int32_t) * starts.size(),
+                           hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(gather_i32_kernel, dim3((unsigned)((starts.size() + 255) / 256)),
+                           dim3(256), 0, s, p->bwd_row, d_st, (int)starts.size(), d_fr);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        e = hipMemcpyAsync(first_row.data(), d_fr, sizeof(int32_t) * starts.size(),
+                           hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        return hipStreamSynchronize(s);
+      }();
+      fr_cleanup();
+      PLAN_TRY(fe);
+    }
+    struct ChunkRef { int64_t row; int b, j; };
+    std::vector<ChunkRef> order_c;
+    {
+      size_t i = 0;
+      for (int b = 0; b < nblocks; ++b)
+        for (int j = 0; j + 1 < (int)cbd[b].size(); ++j)
+          order_c.push_back(ChunkRef{row_pos(first_row[i++]), b, j});
+    }
+    std::stable_sort(order_c.begin(), order_c.end(),
+                     [](const ChunkRef& a, const ChunkRef& b) { return a.row < b.row; });
+    // a block's chunks must come in chunk order (piece numbering, slab regions)
+    std::vector<int32_t> next_chunk((size_t)nblocks, 0);
+    for (ChunkRef& cr : order_c) cr.j = next_chunk[cr.b]++;
     std::vector<int32_t> next_piece((size_t)nblocks, 0);
-    std::vector<std::vector<BwdTask>> per_xcd(kXcds);
-    for (int j = 0; j < nch; ++j) {
-      for (int b = 0; b < nblocks; ++b) {
-        const int32_t e0 = co[(size_t)b * (nch + 1) + j], e1 = co[(size_t)b * (nch + 1) + j + 1];
-        const int np = (int)std::max<int64_t>(1, ((int64_t)e1 - e0 + piece_cap - 1) / piece_cap);
-        for (int q = 0; q < np; ++q) {
-          const int piece = next_piece[b]++;
-          for (int g = 0; g < S; ++g) {  // the groups of a block share its edge stream
-            BwdTask t{};
-            t.col0 = b * C;
-            t.ncols = std::min(C, NC - t.col0);
-            t.e0 = (int32_t)(e0 + ((int64_t)e1 - e0) * q / np);
-            t.e1 = (int32_t)(e0 + ((int64_t)e1 - e0) * (q + 1) / np);
-            t.shared = pieces_of[b] > 1;
-            t.group = g;
-            t.chunk = piece;
-            t.slab = (slab_base[b] >= 0 && piece > 0)
-                         ? (int32_t)(slab_base[b] + (int64_t)(piece - 1) * C * k) : -1;
-            per_xcd[b % kXcds].push_back(t);
-          }
+    std::vector<BwdTask> emitted;
+    for (const ChunkRef& cr : order_c) {
+      const int b = cr.b;
+      const int32_t e0 = cbd[b][cr.j], e1 = cbd[b][cr.j + 1];
+      const int np = npieces((int64_t)e1 - e0);
+      for (int q = 0; q < np; ++q) {
+        const int piece = next_piece[b]++;
+        for (int g = 0; g < S; ++g) {  // the groups of a block share its edge stream
+          BwdTask t{};
+          t.col0 = b * C;
+          t.ncols = std::min(C, NC - t.col0);
+          t.e0 = (int32_t)(e0 + ((int64_t)e1 - e0) * q / np);
+          t.e1 = (int32_t)(e0 + ((int64_t)e1 - e0) * (q + 1) / np);
+          t.shared = pieces_of[b] > 1;
+          t.group = g;
+          t.chunk = piece;
+          t.slab = (slab_base[b] >= 0 && piece > 0)
+                       ? (int32_t)(slab_base[b] + (int64_t)(piece - 1) * C * k) : -1;
+          emitted.push_back(t);
         }
       }
     }
@@ -1041,11 +1706,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
       PLAN_TRY(hipStreamSynchronize(s));
       p->device_bytes += sizeof(int4) * comb.size();
     }
-    size_t len = 0;
-    for (auto& v : per_xcd) len = std::max(len, v.size());
-    btasks.assign(len * kXcds, BwdTask{});  // padding tasks have ncols == 0
-    for (int x = 0; x < kXcds; ++x)
-      for (size_t i = 0; i < per_xcd[x].size(); ++i) btasks[i * kXcds + x] = per_xcd[x][i];
+    // work-group i runs on XCD i % 8 (dealt round-robin; speed only): consecutive tasks of
+    // the emission order spread over the XCDs, and every XCD gets the same share of them
+    btasks = std::move(emitted);
   } else {
     for (int b = 0; b < nblocks; ++b) {
       const int64_t o0 = offs[b], o1 = offs[b + 1];
@@ -1106,6 +1769,15 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                        12ll * kBwdRecPad;
   }
   PLAN_TRY(hipStreamSynchronize(s));
+  // the column order stays with the plan when the backward blocks use it
+  p->col_order = 1;
+  if (order && bcolpos) p->col_order = order_mode;
+  if (order && bcolpos) {
+    p->bwd_corder = order;
+    p->device_bytes += sizeof(int32_t) * (int64_t)NC;
+    order = nullptr;
+  }
+  drop_order();
   dfree(row_of);
   dfree(keys_in);
   dfree(keys_out);
@@ -1131,7 +1803,7 @@ extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* st
   else
     hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
                        (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
-                       nullptr, nullptr, p->bwd_val);
+                       nullptr, nullptr, p->bwd_val, nullptr);
   if (p->fwd_perm)
     hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
                        (hipStream_t)stream, p->fwd_perm, nullptr, nullptr, val, p->num_edges,
@@ -1148,7 +1820,16 @@ extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* st
 }
 
 extern "C" int maxk_plan_get_info(const maxk_plan* p, maxk_plan_info* info) {
-  MAXK_CHECK_ARG(p != nullptr && info != nullptr, "maxk_plan_get_info: null pointer");
+  // the version-1 fields only (a binding of ABI 1 passes a struct that ends at bwd_algo)
+  return maxk_plan_get_info_sized(p, info, (int64_t)offsetof(maxk_plan_info, col_order));
+}
+
+extern "C" int maxk_plan_get_info_sized(const maxk_plan* p, maxk_plan_info* out,
+                                        int64_t info_bytes) {
+  MAXK_CHECK_ARG(p != nullptr && out != nullptr && info_bytes >= 0,
+                 "maxk_plan_get_info: null pointer");
+  maxk_plan_info full{};
+  maxk_plan_info* info = &full;
   info->num_nodes = p->num_nodes;
   info->num_cols = p->num_cols;
   info->num_edges = p->num_edges;
@@ -1162,6 +1843,33 @@ extern "C" int maxk_plan_get_info(const maxk_plan* p, maxk_plan_info* info) {
   info->bwd_shared_blocks = p->n_bwd_shared;
   info->device_bytes = p->device_bytes;
   info->bwd_algo = p->bwd_twopass ? 3 : p->bwd_csc ? 2 : 1;
+  info->col_order = p->col_order;
+  info->bwd_chunk_bounds = (p->bwd_twopass || p->bwd_csc) ? 0 : p->bwd_chunk_mode;
+  info->bwd_tp_chunks = p->bwd_twopass ? p->bwd_tp_chunks : 1;
+  info->bwd_row_order = p->bwd_row_order;
+  info->bwd_workspace_peak = p->bwd_ws_bytes;
+  std::memcpy(out, info, (size_t)std::min<int64_t>(info_bytes, (int64_t)sizeof(maxk_plan_info)));
+  return MAXK_OK;
+}
+
+__global__ void iota_kernel(int n, int32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = i;
+}
+
+extern "C" int maxk_plan_get_col_order(const maxk_plan* p, int32_t* order, void* stream) {
+  MAXK_CHECK_ARG(p != nullptr && (order != nullptr || p->num_cols == 0),
+                 "maxk_plan_get_col_order: null pointer");
+  if (p->num_cols == 0) return MAXK_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (p->bwd_corder) {
+    MAXK_HIP_TRY(hipMemcpyAsync(order, p->bwd_corder, sizeof(int32_t) * (size_t)p->num_cols,
+                                hipMemcpyDeviceToDevice, s));
+  } else {
+    hipLaunchKernelGGL(iota_kernel, dim3((p->num_cols + 255) / 256), dim3(256), 0, s,
+                       p->num_cols, order);
+    MAXK_LAUNCH_CHECK("maxk_plan_get_col_order launch");
+  }
   return MAXK_OK;
 }
 

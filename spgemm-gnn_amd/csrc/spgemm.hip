@@ -106,16 +106,24 @@ __device__ __forceinline__ double fwd_fix_decode(unsigned long long a, double in
 
 // Per task and call: the scale 2^s of the fixed-point forward, or 0 (use f64). fix = {sexp,
 // gexp} from fwd_fix_stats_kernel: every row of the task has sum |val| <= 2^sexp, and every
-// nonzero |val| >= 2^(sexp - gexp). xs = {max |x| bits, 0x7fffffff - min nonzero |x| bits}
-// over the call's sp_data (fwd_xstat_kernel). With 2^ex > max |x| and min |x| >= 2^en:
-// s = 49 - sexp - ex keeps every row's sum of |terms| below 2^49; the rounding error of a term,
-// 2^-(s+1), relative to the smallest possible nonzero term 2^(sexp - gexp + en), is at most
-// 2^(gexp + ex - en - 50). The fixed path is taken when that is <= 2^-25, so every output
-// whose terms do not cancel (|y| >= sum |terms| / 2) is within 2^-24 relative, the rounding of
-// the f32 result itself. Non-finite or all-zero inputs take the f64 path.
-__device__ __forceinline__ double fwd_fix_scale(int2 fix, const uint32_t* xs) {
-  const uint32_t mx = xs[0];
-  const uint32_t mn = 0x7fffffffu - xs[32];
+// nonzero |val| >= 2^(sexp - gexp). The statistics are xs_n pairs {B bits, 0x7fffffff - min
+// nonzero |x| bits} (cbsr_stats_kernel; pair i at xs[i * stride] and xs[i * stride + off2]),
+// where B bounds what one CBSR row adds to one output slot per unit of val: max |x|, or the
+// row's sum |x| when its selectors repeat. With 2^ex > B and min |x| >= 2^en: s = 49 - sexp -
+// ex keeps every slot's sum of |terms| below 2^49 (below 2^50 is what fwd_fix_decode needs);
+// the rounding error of a term, 2^-(s+1), relative to the smallest possible nonzero term
+// 2^(sexp - gexp + en), is at most 2^(gexp + ex - en - 50). The fixed path is taken when that
+// is <= 2^-25, so every output whose terms do not cancel (|y| >= sum |terms| / 2) is within
+// 2^-24 relative, the rounding of the f32 result itself. Non-finite or all-zero inputs take
+// the f64 path.
+__device__ __forceinline__ double fwd_fix_scale(int2 fix, const uint32_t* xs, int xs_n,
+                                                int stride, int off2) {
+  uint32_t mx = 0u, inv = 0u;
+  for (int i = 0; i < xs_n; ++i) {
+    mx = max(mx, xs[i * stride]);
+    inv = max(inv, xs[i * stride + off2]);
+  }
+  const uint32_t mn = 0x7fffffffu - inv;
   if (mx == 0u || mx >= 0x7f800000u || mn == 0u || mn > mx) return 0.0;
   const int ex = (int)(mx >> 23) - 126;                      // max |x| < 2^ex
   const int en = (mn >> 23) ? (int)(mn >> 23) - 127 : -149;  // min |x| >= 2^en
@@ -125,32 +133,54 @@ __device__ __forceinline__ double fwd_fix_scale(int2 fix, const uint32_t* xs) {
   return __builtin_ldexp(1.0, sc);
 }
 
-// max |x| and min nonzero |x| of the call's sp_data (bit patterns of non-negative floats
-// order like integers). st[0] (max) and st[32] (0x7fffffff - min) sit on different cache
-// lines and are zeroed before the launch; a few hundred work-groups reduce in LDS and add
-// one atomic each per word (one atomic per wave on a shared word cost ~190 us at k = 16).
-__global__ __launch_bounds__(256) void fwd_xstat_kernel(const float* __restrict__ x, int64_t n,
-                                                        uint32_t* st) {
+// Statistics of a CBSR table for fwd_fix_scale, one thread per row (bit patterns of
+// non-negative floats order like integers): *st0 = max over rows of the row's slot bound B,
+// *st1 = 0x7fffffff - min nonzero |x|. B is max |x| when the row's nonzero entries have
+// strictly ascending selectors (every exact top-k row), else the row's sum |x| (with 2^-10 of
+// headroom for the f32 sum): m nonzero entries on one selector add m terms to one LDS slot
+// (maxk_hip.h: repeated selectors are summed), which a max |x| bound would not cover. Zero
+// entries (ref_compat padding) add nothing and are skipped. Both words are zeroed before the
+// launch; a few hundred work-groups reduce in LDS and add one atomic each per word (one
+// atomic per wave on a shared word cost ~190 us at k = 16).
+__global__ __launch_bounds__(256) void cbsr_stats_kernel(const float* __restrict__ x,
+                                                         const uint8_t* __restrict__ sel,
+                                                         int64_t nrows, int k, uint32_t* st0,
+                                                         uint32_t* st1) {
   __shared__ uint32_t smx[256 / kWave], smn[256 / kWave];
   uint32_t mx = 0u, mn = 0x7fffffffu;
-  const int64_t n4 = n / 4;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 v = x4[i];
-    const uint32_t b[4] = {__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu,
-                           __float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      mx = max(mx, b[j]);
-      mn = min(mn, b[j] ? b[j] : 0x7fffffffu);
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t mb = 0u, lo = 0x7fffffffu;
+    float sum = 0.f;
+    int prev = -1;
+    bool rep = false;
+    auto take = [&](float v, int s) {
+      const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
+      if (b == 0u) return;
+      mb = max(mb, b);
+      lo = min(lo, b);
+      sum += __uint_as_float(b);
+      rep = rep || s <= prev;
+      prev = s;
+    };
+    const float* xr = x + r * k;
+    const uint8_t* sr = sel + r * k;
+    if ((k & 3) == 0) {
+      for (int l = 0; l < k; l += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + l);
+        const uint32_t s = *reinterpret_cast<const uint32_t*>(sr + l);
+        take(v.x, s & 0xffu);
+        take(v.y, (s >> 8) & 0xffu);
+        take(v.z, (s >> 16) & 0xffu);
+        take(v.w, s >> 24);
+      }
+    } else {
+      for (int l = 0; l < k; ++l) take(xr[l], sr[l]);
     }
-  }
-  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t b = __float_as_uint(x[i]) & 0x7fffffffu;
-    mx = max(mx, b);
-    if (b) mn = min(mn, b);
+    // a non-finite sum (or value) gives bits >= 0x7f800000: fwd_fix_scale falls back
+    const uint32_t rb = rep ? max(mb, __float_as_uint(sum * (1.0f + 0x1p-10f)) & 0x7fffffffu) : mb;
+    mx = max(mx, rb);
+    mn = min(mn, lo);
   }
   for (int o = kWave / 2; o > 0; o >>= 1) {
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
@@ -161,8 +191,8 @@ __global__ __launch_bounds__(256) void fwd_xstat_kernel(const float* __restrict_
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int i = 1; i < 256 / kWave; ++i) { mx = max(mx, smx[i]); mn = min(mn, smn[i]); }
-    atomicMax(&st[0], mx);
-    atomicMax(&st[32], 0x7fffffffu - mn);
+    atomicMax(st0, mx);
+    atomicMax(st1, 0x7fffffffu - mn);
   }
 }
 
@@ -329,7 +359,8 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
     const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
     int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab, int accum,
-    const int2* __restrict__ fix_tab, const uint32_t* __restrict__ xstat) {
+    const int2* __restrict__ fix_tab, const uint32_t* __restrict__ xstat, int xs_n,
+    int xs_stride, int xs_off2) {
   using A = LdsAcc<ACC>;
   using T = typename A::T;
   extern __shared__ __align__(16) double smem_d[];
@@ -361,7 +392,8 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   // fixed-point accumulation for this task (LdsFix), else f64; the 8-byte slots are the same
   double fsc = 0.0;
   if constexpr (VEC == 4 && ACC == MAXK_ACC_F64) {
-    if (fix_tab && !(phase > 0 || accum)) fsc = fwd_fix_scale(fix_tab[ti], xstat);
+    if (fix_tab && !(phase > 0 || accum))
+      fsc = fwd_fix_scale(fix_tab[ti], xstat, xs_n, xs_stride, xs_off2);
   }
   const bool fixed = fsc != 0.0;
   unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(smem_d);
@@ -592,15 +624,16 @@ __global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
 // 32-bit offsets, and the LDS compare-and-swap adds issued as a batch (all reads, then all
 // CAS, then a retry loop for the rare lanes whose CAS lost a race).
 __global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int n, int k, int S,
-                                uint32_t* __restrict__ sel) {
-  // sel[(g * n + c) * L + q] = slots g*k/S + q + L*i, i = 0..3, of column c (L = k / 4S)
+                                uint32_t* __restrict__ sel, const int32_t* __restrict__ corder) {
+  // sel[(g * n + c) * L + q] = slots g*k/S + q + L*i, i = 0..3, of the column at block
+  // position c (corder[c], or c itself) (L = k / 4S)
   const int L = k / (4 * S);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * L * S) return;
   const int g = i / (n * L);
   const int r = i - g * (n * L);
   const int c = r / L, q = r - c * L;
-  const uint8_t* s = sp_index + (size_t)c * k + g * (k / S) + q;
+  const uint8_t* s = sp_index + (size_t)(corder ? corder[c] : c) * k + g * (k / S) + q;
   sel[i] = (uint32_t)s[0] | ((uint32_t)s[L] << 8) | ((uint32_t)s[2 * L] << 16) |
            ((uint32_t)s[3 * L] << 24);
 }
@@ -608,14 +641,14 @@ __global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int n, int
 // Two slots per lane (sspmm_bwd4_kernel<.., F = 2>): sel[(g * n + c) * L + q] = slots
 // g*k/S + q and g*k/S + q + L of column c (L = k / 2S), as one u16.
 __global__ void pack_sel2_kernel(const uint8_t* __restrict__ sp_index, int n, int k, int S,
-                                 uint16_t* __restrict__ sel) {
+                                 uint16_t* __restrict__ sel, const int32_t* __restrict__ corder) {
   const int L = k / (2 * S);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * L * S) return;
   const int g = i / (n * L);
   const int r = i - g * (n * L);
   const int c = r / L, q = r - c * L;
-  const uint8_t* s = sp_index + (size_t)c * k + g * (k / S) + q;
+  const uint8_t* s = sp_index + (size_t)(corder ? corder[c] : c) * k + g * (k / S) + q;
   sel[i] = (uint16_t)(s[0] | (s[L] << 8));
 }
 
@@ -637,7 +670,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
     float* __restrict__ grad_sp, int k, int S, int ncols_all, int KS, int sel_lds,
-    float* __restrict__ slab) {
+    float* __restrict__ slab, const int32_t* __restrict__ corder) {
   extern __shared__ __align__(16) double bsmem[];
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
@@ -831,17 +864,19 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   __syncthreads();
 
   // shared block: global atomics into a zeroed grad_sp, or (slab flush) piece 0 stores into
-  // grad_sp and piece p > 0 into its slab region, summed by bwd_combine_kernel
+  // grad_sp and piece p > 0 into its slab region (block positions), summed by
+  // bwd_combine_kernel; corder maps block positions to the columns of grad_sp
   const bool atomic = t.shared && !slab;
-  float* dst = (slab && t.slab >= 0) ? slab + t.slab + t.group * ns
-                                     : grad_sp + (size_t)t.col0 * k + t.group * ns;
+  const bool to_slab = slab && t.slab >= 0;
+  float* dst = to_slab ? slab + t.slab + t.group * ns : grad_sp + t.group * ns;
   const int n = t.ncols * ns;
   for (int i = threadIdx.x; i < n; i += NT) {
     const int c = i / ns;
     const int l = i - c * ns;
     const float a = bacc[c * KS + (V ? (l % L) * F + l / L : l)];
-    if (atomic) global_add(dst + (size_t)c * k + l, a);
-    else dst[(size_t)c * k + l] = a;
+    const size_t row = to_slab ? (size_t)c : (size_t)(corder ? corder[t.col0 + c] : t.col0 + c);
+    if (atomic) global_add(dst + row * k + l, a);
+    else dst[row * k + l] = a;
   }
 }
 
@@ -856,7 +891,8 @@ template <int U, int NT>
 __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, const uint8_t* __restrict__ sp_index,
-    float* __restrict__ grad_sp, int k, int KS, float* __restrict__ slab) {
+    float* __restrict__ grad_sp, int k, int KS, float* __restrict__ slab,
+    const int32_t* __restrict__ corder) {
   extern __shared__ __align__(16) double bsmem[];
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
@@ -865,13 +901,21 @@ __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
   uint8_t* sell = reinterpret_cast<uint8_t*>(bacc + ((nacc + 3) & ~3));
-  const uint8_t* selg = sp_index + (size_t)t.col0 * k;
+  // the block's selector rows: columns corder[col0 ..] (or col0 .. contiguous)
+  auto col_of = [&](int c) -> size_t { return corder ? (size_t)corder[t.col0 + c] : (size_t)t.col0 + c; };
   const int nsel = t.ncols * k;
   if ((k & 3) == 0) {
-    for (int i = threadIdx.x; i < nsel / 4; i += NT)
-      reinterpret_cast<uint32_t*>(sell)[i] = reinterpret_cast<const uint32_t*>(selg)[i];
+    const int kw = k / 4;
+    for (int i = threadIdx.x; i < nsel / 4; i += NT) {
+      const int c = i / kw;
+      reinterpret_cast<uint32_t*>(sell)[i] =
+          reinterpret_cast<const uint32_t*>(sp_index + col_of(c) * k)[i - c * kw];
+    }
   } else {
-    for (int i = threadIdx.x; i < nsel; i += NT) sell[i] = selg[i];
+    for (int i = threadIdx.x; i < nsel; i += NT) {
+      const int c = i / k;
+      sell[i] = sp_index[col_of(c) * k + (i - c * k)];
+    }
   }
   __syncthreads();
 
@@ -945,12 +989,13 @@ __global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
   __syncthreads();
 
   const bool atomic = t.shared && !slab;
-  float* dst = (slab && t.slab >= 0) ? slab + t.slab : grad_sp + (size_t)t.col0 * k;
+  const bool to_slab = slab && t.slab >= 0;
   for (int i = threadIdx.x; i < nsel; i += NT) {
     const int c = i / k;
     const float a = bacc[c * KS + (i - c * k)];
-    if (atomic) global_add(dst + i, a);
-    else dst[i] = a;
+    float* dst = to_slab ? slab + t.slab + i : grad_sp + col_of(c) * k + (i - c * k);
+    if (atomic) global_add(dst, a);
+    else *dst = a;
   }
 }
 
@@ -964,15 +1009,21 @@ constexpr int kCombineSlice = 1024;
 __global__ __launch_bounds__(256) void bwd_combine_kernel(float* __restrict__ grad_sp,
                                                           const float* __restrict__ slab,
                                                           const int4* __restrict__ comb, int k,
-                                                          int region_floats) {
+                                                          int region_floats,
+                                                          const int32_t* __restrict__ corder) {
   const int4 cb = comb[blockIdx.y];
   const int n = min(cb.w * k, (int)(blockIdx.x + 1) * kCombineSlice);
   const int i0 = blockIdx.x * kCombineSlice;
-  float* g = grad_sp + (size_t)cb.z * k;
+  // element i of the block (position cb.z + i / k) lives in grad_sp row corder[position]
+  auto gp = [&](int i) -> float* {
+    const int c = i / k;
+    return grad_sp + (size_t)(corder ? corder[cb.z + c] : cb.z + c) * k + (i - c * k);
+  };
   const float* sl = slab + cb.x;
   if ((k & 3) == 0) {
     for (int i = i0 + threadIdx.x * 4; i < n; i += 256 * 4) {
-      float4 a = *reinterpret_cast<const float4*>(g + i);
+      float* g = gp(i);  // k % 4 == 0: the 4 elements share a column
+      float4 a = *reinterpret_cast<const float4*>(g);
       for (int j = 0; j < cb.y; ++j) {
         const float4 b = *reinterpret_cast<const float4*>(sl + (size_t)j * region_floats + i);
         a.x += b.x;
@@ -980,13 +1031,14 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(float* __restrict__ gr
         a.z += b.z;
         a.w += b.w;
       }
-      *reinterpret_cast<float4*>(g + i) = a;
+      *reinterpret_cast<float4*>(g) = a;
     }
   } else {
     for (int i = i0 + threadIdx.x; i < n; i += 256) {
-      float a = g[i];
+      float* g = gp(i);
+      float a = *g;
       for (int j = 0; j < cb.y; ++j) a += sl[(size_t)j * region_floats + i];
-      g[i] = a;
+      *g = a;
     }
   }
 }
@@ -1079,13 +1131,16 @@ template <int U, int R, bool CS = false>
 __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
     const int32_t* __restrict__ ptr, const uint32_t* __restrict__ erec,
     const float* __restrict__ G, const uint8_t* __restrict__ sp_index, float* __restrict__ T,
-    int N, int D, int k, const int32_t* __restrict__ pos) {
-  // R rows of kMaxDim floats per wavefront (any u8 selector stays inside the wave's rows)
+    int rbeg, int rend, int64_t ebase, int D, int k, const int32_t* __restrict__ pos) {
+  // R rows of kMaxDim floats per wavefront (any u8 selector stays inside the wave's rows).
+  // This launch covers destination rows [rbeg, rend), whose edges [ptr[rbeg], ptr[rend])
+  // have their slots at T + (e - ebase) * k (one row chunk of the workspace)
   __shared__ float grow[256 / kWave][R * kMaxDim];
   const int lane = threadIdx.x & (kWave - 1);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int r0 = (blockIdx.x * (256 / kWave) + w) * R;
-  if (r0 >= N) return;
+  const int r0 = rbeg + (blockIdx.x * (256 / kWave) + w) * R;
+  if (r0 >= rend) return;
+  const int N = rend;
   const int r1 = min(N, r0 + R);
   const int e0 = __builtin_amdgcn_readfirstlane(ptr[r0]);
   const int e1 = __builtin_amdgcn_readfirstlane(ptr[r1]);
@@ -1119,7 +1174,8 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
   // branchless: idle slots load the row's last edge again and their stores fall outside the
   // row's buffer range (dropped), so every load of a step is in flight together
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
-      T + (size_t)e0 * k, (short)0, (int)((uint32_t)(e1 - e0) * (uint32_t)k * 4u), 0x00020000);
+      T + (size_t)(e0 - ebase) * k, (short)0, (int)((uint32_t)(e1 - e0) * (uint32_t)k * 4u),
+      0x00020000);
   for (int base = e0; base < e1; base += EPS * U) {
     uint32_t c[U];
     float v[U];
@@ -1168,13 +1224,16 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
 }
 
 // Two-pass backward, pass 2: one wavefront per column c sums the slots of the column's
-// in-edges perm[colptr[c] .. colptr[c+1]) (64/L slots per step, float4 per lane), reduces
-// over the slots with shuffles and stores grad_sp[c] (every column written once: no memset,
-// no atomics).
+// in-edges perm[lo[c] .. hi[c]) (64/L slots per step, float4 per lane), reduces over the
+// slots with shuffles and stores grad_sp[c] (every column written once: no memset, no
+// atomics). Row chunks (plan->bwd_tp_chunks > 1): this pass covers the in-edges of one row
+// chunk, whose slots are at T + (perm - ebase) * k; chunk 0 stores, later chunks add to the
+// stored sums in chunk order (deterministic).
 template <int U, bool CS = false>
 __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
-    const int32_t* __restrict__ colptr, const int32_t* __restrict__ perm,
-    const float* __restrict__ T, float* __restrict__ grad_sp, int ncols, int k) {
+    const int32_t* __restrict__ lo, const int32_t* __restrict__ hi,
+    const int32_t* __restrict__ perm, const float* __restrict__ T, int64_t ebase,
+    float* __restrict__ grad_sp, int ncols, int k, int accumulate) {
   const int lane = threadIdx.x & (kWave - 1);
   const int c = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
   if (c >= ncols) return;
@@ -1182,14 +1241,14 @@ __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
   const int EPS = kWave / L;
   const int slot = lane / L;
   const int q = lane - slot * L;
-  const int e0 = colptr[c], e1 = colptr[c + 1];
+  const int e0 = lo[c], e1 = hi[c];
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int base = e0; base < e1; base += EPS * U) {
     int32_t pe[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = min(base + u * EPS + slot, e1 - 1);
-      pe[u] = CS ? j : perm[j];  // CS: the slots are already in column order
+      pe[u] = CS ? j : (int32_t)(perm[j] - ebase);  // CS: the slots are already in column order
     }
     float4 t[U];
 #pragma unroll
@@ -1213,7 +1272,17 @@ __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
     acc.z += __shfl_xor(acc.z, m, kWave);
     acc.w += __shfl_xor(acc.w, m, kWave);
   }
-  if (slot == 0) *reinterpret_cast<float4*>(grad_sp + (size_t)c * k + 4 * q) = acc;
+  if (slot == 0) {
+    float4* dst = reinterpret_cast<float4*>(grad_sp + (size_t)c * k + 4 * q);
+    if (accumulate) {
+      const float4 o = *dst;
+      acc.x += o.x;
+      acc.y += o.y;
+      acc.z += o.z;
+      acc.w += o.w;
+    }
+    *dst = acc;
+  }
 }
 
 // Dense CSR SpMM (DGL update_all(copy_u, sum) with edge weights: the ReLU layers' dense
@@ -1304,8 +1373,11 @@ static int check_plan(const maxk_plan* plan, const int32_t* ptr, const int32_t* 
 static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const int32_t* idx,
                                const float* val, const float* sp_data, const uint8_t* sp_index,
                                float* out, int32_t N, int64_t E, int32_t k, int32_t D,
-                               void* stream, int accum, void* ws, int64_t ws_bytes) {
+                               void* stream, int accum, void* ws, int64_t ws_bytes,
+                               const uint32_t* stats = nullptr, int n_stats = 0) {
   MAXK_CHECK_ARG(N >= 0 && E >= 0, "maxk_spgemm_forward: negative size");
+  MAXK_CHECK_ARG(stats == nullptr || (n_stats >= 1 && n_stats <= 1024),
+                 "maxk_spgemm_forward_ex: n_stats must be in [1, 1024]");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_spgemm_forward: dim_origin must be in [1, 256]");
   MAXK_CHECK_ARG(k >= 1 && k <= D, "k must be between 1 and input dimension");
   int rc = check_plan(plan, ptr, idx, N, E, k, D, "maxk_spgemm_forward");
@@ -1354,17 +1426,28 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
                        rec_ws, plan->num_cols, k, rec_bytes);
     MAXK_LAUNCH_CHECK("pack_cbsr launch");
   }
-  // fixed-point forward: the call's max / min |x| for fwd_fix_scale (one pass over sp_data)
+  // fixed-point forward: the call's slot bound / min |x| for fwd_fix_scale (one pass over the
+  // CBSR table), or the caller's per-rank pairs (maxk_spgemm_forward_ex)
   const int2* fix_tab = nullptr;
-  uint32_t* xstat = nullptr;
+  const uint32_t* xstat = nullptr;
+  int xs_n = 1, xs_stride = 0, xs_off2 = 32;
   if (plan->fwd_fix && !accum && plan->num_cols > 0) {
     fix_tab = plan->fwd_fix;
-    xstat = reinterpret_cast<uint32_t*>(ws_base + plan->fwd_xstat_off);
-    MAXK_HIP_TRY(hipMemsetAsync(xstat, 0, 256, s));
-    const int64_t nx = (int64_t)plan->num_cols * k;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nx + 4095) / 4096, 2 * plan->cus));
-    hipLaunchKernelGGL(fwd_xstat_kernel, dim3(grid), dim3(256), 0, s, sp_data, nx, xstat);
-    MAXK_LAUNCH_CHECK("fwd_xstat launch");
+    if (stats) {
+      xstat = stats;
+      xs_n = n_stats;
+      xs_stride = 2;
+      xs_off2 = 1;
+    } else {
+      uint32_t* st = reinterpret_cast<uint32_t*>(ws_base + plan->fwd_xstat_off);
+      MAXK_HIP_TRY(hipMemsetAsync(st, 0, 256, s));
+      const int64_t nr = plan->num_cols;
+      const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nr + 255) / 256, 2 * plan->cus));
+      hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nr, k,
+                         st, st + 32);
+      MAXK_LAUNCH_CHECK("cbsr_stats launch");
+      xstat = st;
+    }
   }
   const int rot = plan->fwd_rot_ticks;
   // persistent grid: as many work-groups as fit on the device at once (capped by tasks)
@@ -1381,7 +1464,8 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU, NT, FL>), dim3(g), dim3(NT), lds, s, \
                          plan->fwd_tasks, plan->n_fwd_tasks, plan->fwd_phase_off, B, b,   \
                          plan->fwd_cv, sp_data, sp_index, recp,                           \
-                         rec_bytes_eff, out, D, k, R, rot, seltab, accum, fix_tab, xstat); \
+                         rec_bytes_eff, out, D, k, R, rot, seltab, accum, fix_tab, xstat, \
+                         xs_n, xs_stride, xs_off2);                                       \
   } while (0)
 #define FWD_LAUNCH(V, A)                                                                  \
   do {                                                                                    \
@@ -1473,6 +1557,40 @@ extern "C" int maxk_spgemm_forward_ws(const maxk_plan* plan, const int32_t* ptr,
                              accumulate, workspace, workspace_bytes);
 }
 
+extern "C" int maxk_spgemm_forward_ex(const maxk_plan* plan, const int32_t* ptr,
+                                      const int32_t* idx, const float* val,
+                                      const float* sp_data, const uint8_t* sp_index, float* out,
+                                      int32_t N, int64_t E, int32_t k, int32_t D,
+                                      int32_t accumulate, const uint32_t* stats,
+                                      int32_t n_stats, void* workspace,
+                                      int64_t workspace_bytes, void* stream) {
+  MAXK_CHECK_ARG(accumulate == 0 || accumulate == 1,
+                 "maxk_spgemm_forward_ex: accumulate must be 0 or 1");
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream,
+                             accumulate, workspace, workspace_bytes, stats, n_stats);
+}
+
+extern "C" int maxk_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int32_t num_rows,
+                               int32_t dim_k, uint32_t* stats, void* stream) {
+  MAXK_CHECK_ARG(num_rows >= 0 && dim_k >= 1 && dim_k <= kMaxDim,
+                 "maxk_cbsr_stats: bad size");
+  MAXK_CHECK_ARG(stats != nullptr && (num_rows == 0 || (sp_data && sp_index)),
+                 "maxk_cbsr_stats: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  MAXK_HIP_TRY(hipMemsetAsync(stats, 0, 2 * sizeof(uint32_t), s));
+  if (num_rows == 0) return MAXK_OK;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((num_rows + 255) / 256, 2 * cus));
+  hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
+                     (int64_t)num_rows, dim_k, stats, stats + 1);
+  MAXK_LAUNCH_CHECK("maxk_cbsr_stats launch");
+  return MAXK_OK;
+}
+
 extern "C" int maxk_spgemm_forward_acc(const maxk_plan* plan, const int32_t* ptr,
                                        const int32_t* idx, const float* val,
                                        const float* sp_data, const uint8_t* sp_index,
@@ -1515,41 +1633,51 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     const int slices = (plan->bwd_block_cols * k + kCombineSlice - 1) / kCombineSlice;
     hipLaunchKernelGGL(bwd_combine_kernel, dim3(slices, plan->n_bwd_combine), dim3(256), 0,
                        (hipStream_t)stream, grad_sp, slab, plan->bwd_combine, k,
-                       plan->bwd_block_cols * k);
+                       plan->bwd_block_cols * k, plan->bwd_corder);
     MAXK_LAUNCH_CHECK("bwd_combine launch");
     return MAXK_OK;
   };
   hipStream_t s = (hipStream_t)stream;
   if (plan->bwd_twopass) {
-    // the plan checked k % 4 == 0, k / 4 a power of two <= 64, E > 0, NC > 0
+    // the plan checked k % 4 == 0, k / 4 a power of two <= 64, E > 0, NC > 0; per row chunk
+    // (the workspace holds one chunk's products): row pass, then column pass
     const int R = plan->bwd_tp_rows;
-    const dim3 rgrid((N + 4 * R - 1) / (4 * R));
-    const bool cs = plan->bwd_tp_csc;
+    const bool cs = plan->bwd_tp_csc;  // the plan allows it with one chunk only
+    const int P = plan->bwd_tp_chunks;
+    const int NC = plan->num_cols;
+    for (int p = 0; p < P; ++p) {
+      const int rb = plan->tp_rows[p], re = plan->tp_rows[p + 1];
+      const int64_t eb = plan->tp_edges[p];
+      if (re > rb) {
+        const dim3 rgrid((re - rb + 4 * R - 1) / (4 * R));
 #define ROWS_LAUNCH(RR)                                                                   \
-    do {                                                                                  \
-      if (cs)                                                                             \
-        hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR, true>), rgrid, dim3(256), 0, s,  \
-                           ptr, plan->bwd_erec, grad_out, sp_index, tbuf_ws, N, D, k,     \
-                           plan->bwd_perm);                                               \
-      else                                                                                \
-        hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR>), rgrid, dim3(256), 0, s, ptr,   \
-                           plan->bwd_erec, grad_out, sp_index, tbuf_ws, N, D, k, nullptr); \
-    } while (0)
-    if (R >= 8) ROWS_LAUNCH(8);
-    else if (R == 4) ROWS_LAUNCH(4);
-    else if (R == 2) ROWS_LAUNCH(2);
-    else ROWS_LAUNCH(1);
+        do {                                                                              \
+          if (cs)                                                                         \
+            hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR, true>), rgrid, dim3(256), 0, s, \
+                               ptr, plan->bwd_erec, grad_out, sp_index, tbuf_ws, rb, re,  \
+                               eb, D, k, plan->bwd_perm);                                 \
+          else                                                                            \
+            hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR>), rgrid, dim3(256), 0, s, ptr, \
+                               plan->bwd_erec, grad_out, sp_index, tbuf_ws, rb, re, eb, D, \
+                               k, nullptr);                                               \
+        } while (0)
+        if (R >= 8) ROWS_LAUNCH(8);
+        else if (R == 4) ROWS_LAUNCH(4);
+        else if (R == 2) ROWS_LAUNCH(2);
+        else ROWS_LAUNCH(1);
 #undef ROWS_LAUNCH
-    MAXK_LAUNCH_CHECK("sspmm_bwd_rows launch");
-    if (cs)
-      hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4, true>), dim3((plan->num_cols + 3) / 4),
-                         dim3(256), 0, s, plan->bwd_colptr, nullptr, tbuf_ws, grad_sp,
-                         plan->num_cols, k);
-    else
-      hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4>), dim3((plan->num_cols + 3) / 4), dim3(256),
-                         0, s, plan->bwd_colptr, plan->bwd_perm, tbuf_ws, grad_sp,
-                         plan->num_cols, k);
-    MAXK_LAUNCH_CHECK("sspmm_bwd_cols launch");
+        MAXK_LAUNCH_CHECK("sspmm_bwd_rows launch");
+      }
+      const int32_t* lo = P > 1 ? plan->bwd_colptr2 + (size_t)p * NC : plan->bwd_colptr;
+      const int32_t* hi = P > 1 ? plan->bwd_colptr2 + (size_t)(p + 1) * NC : plan->bwd_colptr + 1;
+      if (cs)
+        hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4, true>), dim3((NC + 3) / 4), dim3(256), 0, s,
+                           lo, hi, nullptr, tbuf_ws, (int64_t)0, grad_sp, NC, k, 0);
+      else
+        hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4>), dim3((NC + 3) / 4), dim3(256), 0, s, lo,
+                           hi, plan->bwd_perm, tbuf_ws, eb, grad_sp, NC, k, p > 0 ? 1 : 0);
+      MAXK_LAUNCH_CHECK("sspmm_bwd_cols launch");
+    }
     return MAXK_OK;
   }
   if (plan->bwd_csc) {
@@ -1557,7 +1685,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     if (F == 4) {
       const int nsel = plan->num_cols * (k / 4);
       hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
-                         plan->num_cols, k, 1, sel_ws);
+                         plan->num_cols, k, 1, sel_ws, nullptr);
     }
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
     const dim3 cgrid((plan->num_cols + 3) / 4);
@@ -1591,7 +1719,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       if (lds1 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd1_kernel<UU, NT>, lds1));     \
       hipLaunchKernelGGL((sspmm_bwd1_kernel<UU, NT>), grid, dim3(NT), lds1, s,            \
                          plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sp_index,     \
-                         grad_sp, k, plan->bwd_ks, slab);                                 \
+                         grad_sp, k, plan->bwd_ks, slab, plan->bwd_corder);              \
     } while (0)
     const int W = plan->bwd_waves, U = plan->bwd_unroll;
     if (W == 16) BWD1_LAUNCH(16, 1024);
@@ -1609,7 +1737,8 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     const int S = plan->bwd_slot_groups;
     const int nsel = plan->num_cols * (k / 2);
     hipLaunchKernelGGL(pack_sel2_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
-                       plan->num_cols, k, S, reinterpret_cast<uint16_t*>(sel_ws));
+                       plan->num_cols, k, S, reinterpret_cast<uint16_t*>(sel_ws),
+                       plan->bwd_corder);
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
     const size_t lds2 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
                         (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
@@ -1620,7 +1749,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, false, V, Q, 2>), grid, dim3(NT), lds2, s, \
                          plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sel_ws,       \
                          grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds,  \
-                         slab);                                                           \
+                         slab, plan->bwd_corder);                                         \
     } while (0)
     const int U = plan->bwd_unroll;
     const bool QL = plan->bwd_quad && (k / S / 2) % 4 == 0;
@@ -1647,7 +1776,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     const int S = plan->bwd_slot_groups;
     const int nsel = plan->num_cols * (k / 4);
     hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
-                       plan->num_cols, k, S, sel_ws);
+                       plan->num_cols, k, S, sel_ws, plan->bwd_corder);
     const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
     const size_t lds4 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
                         (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
@@ -1657,7 +1786,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF, V, Q>), grid, dim3(NT), lds4, s,  \
                          plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sel_ws, \
                          grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds,  \
-                         slab);                                                           \
+                         slab, plan->bwd_corder);                                         \
     } while (0)
     const int W = plan->bwd_waves, U = plan->bwd_unroll;
     const bool PFon = plan->bwd_prefetch != 0;

@@ -17,11 +17,13 @@ from ._lib import LIB_PATH, MaxKError, lib  # noqa: F401  (loads libmaxk_hip.so)
 from .ops import (  # noqa: F401
     TOPK_MODES,
     GraphPlan,
+    cbsr_stats,
     clear_plan_cache,
     dense_spmm,
     get_plan,
     maxk_backward,
     maxk_forward,
+    plan_col_order,
     spgemm_backward,
     spgemm_forward,
 )
@@ -48,7 +50,7 @@ from .layers import (  # noqa: F401,E402
 
 __all__ = [
     "maxk_forward", "maxk_backward", "spgemm_forward", "spgemm_backward",
-    "dense_spmm", "GraphPlan", "get_plan", "clear_plan_cache", "CSRGraph",
+    "dense_spmm", "cbsr_stats", "plan_col_order", "GraphPlan", "get_plan", "clear_plan_cache", "CSRGraph",
     "MaxKFunction", "SpGEMMFunction", "maxk", "spgemm", "maxk_aggregate", "MaxKError",
     "densify", "MaxKSAGEConv", "MaxKGCNConv", "MaxKGINConv", "MaxKSAGE", "MaxKGCN",
     "MaxKGIN", "dense_aggregate", "DenseAggFunction",

@@ -32,8 +32,15 @@ SIGNATURES = {
                                              _vp, ctypes.POINTER(_vp)]),
     "maxk_plan_create_ex": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _vp,
                                            _vp, ctypes.POINTER(_vp)]),
+    "maxk_plan_create_sized": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32,
+                                              _vp, _i64, _vp, _vp, ctypes.POINTER(_vp)]),
     "maxk_plan_refresh_values": (ctypes.c_int, [_vp, _vp, _vp]),
     "maxk_plan_get_info": (ctypes.c_int, [_vp, _vp]),
+    "maxk_plan_get_info_sized": (ctypes.c_int, [_vp, _vp, _i64]),
+    "maxk_plan_get_col_order": (ctypes.c_int, [_vp, _vp, _vp]),
+    "maxk_cbsr_stats": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp]),
+    "maxk_spgemm_forward_ex": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
+                                              _i32, _i32, _i32, _vp, _i32, _vp, _i64, _vp]),
     "maxk_plan_destroy": (ctypes.c_int, [_vp]),
     "maxk_spgemm_forward": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
                                            _i32, _i32, _vp]),
@@ -92,10 +99,17 @@ class PlanOptions(ctypes.Structure):
         ("bwd_chunk_bounds", _i32),
         ("fwd_fixed", _i32),
         ("bwd_tp_store", _i32),
+        # ABI 2 (maxk_plan_create_sized)
+        ("bwd_row_cost", _i32),
+        ("col_order", _i32),
+        ("bwd_tp_chunks", _i32),
+        ("bwd_row_order", _i32),
     ]
 
 
 ACC_KINDS = {"auto": 0, "f64": 1, "f32_cas": 2}
+# maxk_plan_options.col_order by name
+COL_ORDERS = {"auto": 0, "identity": 1, "scattered": 2, "clustered": 3, "given": 4}
 
 
 class PlanInfo(ctypes.Structure):
@@ -115,6 +129,12 @@ class PlanInfo(ctypes.Structure):
         ("device_bytes", _i64),
         ("num_cols", _i32),
         ("bwd_algo", _i32),
+        # ABI 2 (maxk_plan_get_info_sized)
+        ("col_order", _i32),
+        ("bwd_chunk_bounds", _i32),
+        ("bwd_tp_chunks", _i32),
+        ("bwd_row_order", _i32),
+        ("bwd_workspace_peak", _i64),
     ]
 
     def as_dict(self):

@@ -24,7 +24,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import ACC_KINDS, PlanInfo, PlanOptions, check, lib
+from ._lib import ACC_KINDS, COL_ORDERS, PlanInfo, PlanOptions, check, lib
 
 TOPK_MODES = {"exact": 0, "ref_compat": 1}
 
@@ -141,7 +141,12 @@ class GraphPlan:
     """
 
     def __init__(self, ptr, idx, val, num_nodes, num_edges, dim_origin, dim_k,
-                 num_cols: Optional[int] = None, options: Optional[dict] = None):
+                 num_cols: Optional[int] = None, options: Optional[dict] = None,
+                 col_order: Optional[torch.Tensor] = None):
+        """``options``: ``maxk_plan_options`` fields by name (``col_order`` also by name:
+        'identity', 'scattered', 'clustered'); ``col_order``: an int32 device permutation of
+        the columns (position -> column) for the backward's column blocks, which selects
+        ``col_order='given'``."""
         self.handle = ctypes.c_void_p(0)
         self.device = ptr.device
         self._refs = (ptr, idx, val)  # keep the graph's storage alive while cached
@@ -156,12 +161,19 @@ class GraphPlan:
         for key, value in (options or {}).items():
             if key in ("fwd_accumulator", "bwd_accumulator") and isinstance(value, str):
                 value = ACC_KINDS[value]
+            if key == "col_order" and isinstance(value, str):
+                value = COL_ORDERS[value]
             setattr(opts, key, int(value))
+        if col_order is not None:
+            _check_tensor(col_order, "col_order", torch.int32)
+            _need(col_order.numel() == self.num_cols, "col_order must have num_cols entries")
+            opts.col_order = COL_ORDERS["given"]
         with torch.cuda.device(ptr.device):
-            check(lib.maxk_plan_create_ex(_p(ptr), _p(idx), _p(val), self.num_rows,
-                                          self.num_cols, self.num_edges, self.dim_origin,
-                                          self.dim_k, ctypes.byref(opts), _stream(),
-                                          ctypes.byref(self.handle)), "maxk_plan_create")
+            check(lib.maxk_plan_create_sized(_p(ptr), _p(idx), _p(val), self.num_rows,
+                                             self.num_cols, self.num_edges, self.dim_origin,
+                                             self.dim_k, ctypes.byref(opts),
+                                             ctypes.sizeof(opts), _p(col_order), _stream(),
+                                             ctypes.byref(self.handle)), "maxk_plan_create")
         fb, bb = ctypes.c_int64(0), ctypes.c_int64(0)
         check(lib.maxk_plan_workspace_bytes(self.handle, ctypes.byref(fb), ctypes.byref(bb)),
               "maxk_plan_workspace_bytes")
@@ -186,11 +198,27 @@ class GraphPlan:
     def _workspace(self, nbytes):
         if not self.external or nbytes == 0:
             return None, 0
-        return torch.empty(nbytes, dtype=torch.uint8, device=self.device), nbytes
+        try:
+            return torch.empty(nbytes, dtype=torch.uint8, device=self.device), nbytes
+        except torch.OutOfMemoryError:
+            # the two-pass backward's product workspace is the large one (one row chunk of
+            # E x k x 4 bytes, <= 4 GiB by default): give the allocator its cached blocks
+            # back once, then say which knob bounds it
+            torch.cuda.empty_cache()
+            try:
+                return torch.empty(nbytes, dtype=torch.uint8, device=self.device), nbytes
+            except torch.OutOfMemoryError as exc:
+                raise torch.OutOfMemoryError(
+                    f"maxk_kernels: per-call workspace of {nbytes} bytes does not fit; a plan "
+                    f"built with options={{'bwd_tp_chunks': P}} (more row chunks) or "
+                    f"{{'bwd_algo': 1}} (column blocks) needs less") from exc
 
-    def forward(self, sp_data, sp_index, out=None, accumulate: bool = False) -> torch.Tensor:
+    def forward(self, sp_data, sp_index, out=None, accumulate: bool = False,
+                stats: Optional[torch.Tensor] = None) -> torch.Tensor:
         """SpGEMM with this plan: sp tables [num_cols, k] -> out [num_rows, D];
-        ``accumulate=True`` adds into the given ``out`` instead of overwriting it."""
+        ``accumulate=True`` adds into the given ``out`` instead of overwriting it. ``stats``:
+        int32 [n, 2] fixed-point statistics covering the table (:func:`cbsr_stats` per
+        part; the multi-GPU path gathers one pair per rank) instead of a pass over it."""
         ptr, idx, val = self._refs
         if out is None:
             if accumulate:
@@ -200,10 +228,15 @@ class GraphPlan:
         stream = torch.cuda.current_stream(self.device)
         self._begin(stream)
         ws, wsb = self._workspace(self.fwd_ws_bytes)
-        check(lib.maxk_spgemm_forward_ws(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
+        if stats is not None:
+            _need(stats.is_cuda and stats.is_contiguous() and stats.dtype == torch.int32 and
+                  stats.dim() == 2 and stats.shape[1] == 2 and stats.shape[0] >= 1,
+                  "stats must be a contiguous int32 [n, 2] CUDA tensor")
+        check(lib.maxk_spgemm_forward_ex(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
                                          _p(sp_index), _p(out), self.num_rows, self.num_edges,
-                                         self.dim_k, self.dim_origin, int(accumulate), _p(ws),
-                                         wsb, ctypes.c_void_p(stream.cuda_stream)),
+                                         self.dim_k, self.dim_origin, int(accumulate),
+                                         _p(stats), 0 if stats is None else stats.shape[0],
+                                         _p(ws), wsb, ctypes.c_void_p(stream.cuda_stream)),
               "spgemm_forward")
         self._end(stream)
         return out
@@ -247,7 +280,8 @@ class GraphPlan:
 
     def info(self) -> dict:
         info = PlanInfo()
-        check(lib.maxk_plan_get_info(self.handle, ctypes.byref(info)), "maxk_plan_get_info")
+        check(lib.maxk_plan_get_info_sized(self.handle, ctypes.byref(info), ctypes.sizeof(info)),
+              "maxk_plan_get_info")
         d = info.as_dict()
         d["fwd_workspace_bytes"] = self.fwd_ws_bytes
         d["bwd_workspace_bytes"] = self.bwd_ws_bytes
@@ -378,12 +412,45 @@ def spgemm_backward(ptr, idx, val, grad_output, sp_index, num_nodes: int, num_ed
     return grad_sp
 
 
+def plan_col_order(plan: GraphPlan) -> torch.Tensor:
+    """The plan's column order: int32 [num_cols], position -> column of the backward's column
+    blocks (the identity for plans without one)."""
+    out = torch.empty(plan.num_cols, dtype=torch.int32, device=plan.device)
+    with torch.cuda.device(plan.device):
+        check(lib.maxk_plan_get_col_order(plan.handle, _p(out), _stream()), "plan_col_order")
+    return out
+
+
+def cbsr_stats(sp_data: torch.Tensor, sp_index: torch.Tensor,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fixed-point statistics of a CBSR table (``maxk_cbsr_stats``): int32 [1, 2] (written
+    into ``out`` when given), the pair :meth:`GraphPlan.forward` takes as ``stats``."""
+    _check_tensor(sp_data, "sp_data", torch.float32)
+    _check_tensor(sp_index, "sp_index", torch.uint8)
+    _need(sp_data.dim() == 2 and sp_index.shape == sp_data.shape,
+          "sp_data and sp_index must be [N, k]")
+    if out is None:
+        out = torch.empty((1, 2), dtype=torch.int32, device=sp_data.device)
+    _need(out.is_cuda and out.is_contiguous() and out.dtype == torch.int32 and out.numel() == 2,
+          "out must be a contiguous int32 CUDA tensor of 2 elements")
+    with torch.cuda.device(sp_data.device):
+        check(lib.maxk_cbsr_stats(_p(sp_data), _p(sp_index), sp_data.shape[0], sp_data.shape[1],
+                                  _p(out), _stream()), "cbsr_stats")
+    return out
+
+
 def dense_spmm(ptr, idx, val, x) -> torch.Tensor:
-    """Dense CSR SpMM comparator (DGL ``update_all(copy_u, sum)`` with edge weights)."""
+    """Dense CSR SpMM comparator (DGL ``update_all(copy_u, sum)`` with edge weights). The
+    kernel takes float4 rows: other widths run on a copy padded to a multiple of 4 features
+    (zeros; DGL's SAGEConv/GraphConv/GINConv accept any hidden size)."""
     _check_tensor(x, "x", torch.float32)
     _check_graph(ptr, idx, val, x.shape[0], idx.numel())
-    y = torch.empty_like(x)
+    _need(x.dim() == 2, "x must be 2D")
+    d = x.shape[1]
+    d4 = (d + 3) // 4 * 4
+    xin = x if d4 == d else torch.nn.functional.pad(x, (0, d4 - d)).contiguous()
+    y = torch.empty_like(xin)
     with torch.cuda.device(x.device):
-        check(lib.maxk_dense_spmm_csr(_p(ptr), _p(idx), _p(val), _p(x), _p(y), x.shape[0],
-                                      x.shape[1], _stream()), "dense_spmm")
-    return y
+        check(lib.maxk_dense_spmm_csr(_p(ptr), _p(idx), _p(val), _p(xin), _p(y), x.shape[0],
+                                      d4, _stream()), "dense_spmm")
+    return y if d4 == d else y[:, :d].contiguous()

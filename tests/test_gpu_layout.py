@@ -1,0 +1,268 @@
+"""GPU: the ABI-2 layout options against the oracle.
+
+* column orders of the backward's column blocks (identity / scattered / clustered / the
+  caller's permutation) and the chunk bounds (equal edges / equal cost), on graphs with and
+  without community structure in ID order;
+* row chunks of the two-pass backward (bounded workspace);
+* the fixed-point forward's bound with repeated selectors (maxk_hip.h: repeated selectors in
+  one CBSR row are summed) and the per-part statistics of maxk_spgemm_forward_ex;
+* the dense comparator at hidden sizes that are not a multiple of 4;
+* maxk_plan_get_info writes only the version-1 struct.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import maxk_kernels as mk
+from maxk_kernels import _lib, graphs
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def assert_close(got, ref, mag, rtol=RTOL):
+    got = got.detach().cpu().numpy() if torch.is_tensor(got) else got
+    ok, worst = oracle.close_enough(got, ref, mag, rtol=rtol)
+    assert ok, f"worst err/bound = {worst:.3g}"
+
+
+def community(n=12_000, e=600_000, shuffle=False, seed=71):
+    p, i = graphs.community_csr(n, e, communities=9, seed=seed, shuffle=shuffle)
+    return p.numpy(), i.numpy(), graphs.gcn_values(p, i).numpy()
+
+
+_GRAPHS = {}
+
+
+def graph(name):
+    if name not in _GRAPHS:
+        if name == "uniform":
+            p, i = graphs.synthetic_csr(12_000, 600_000, seed=72)
+            _GRAPHS[name] = (p.numpy(), i.numpy(), graphs.sage_mean_values(p).numpy())
+        else:
+            _GRAPHS[name] = community(shuffle=name == "community_shuffled")
+    return _GRAPHS[name]
+
+
+def dev(a, gpu):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+@pytest.mark.parametrize("gname", ["uniform", "community", "community_shuffled"])
+@pytest.mark.parametrize("order", ["identity", "scattered", "clustered"])
+@pytest.mark.parametrize("bounds", [2, 3])
+@pytest.mark.parametrize("k", [8, 16, 32])
+@pytest.mark.parametrize("rows", [1, 2])
+def test_col_order_and_chunk_bounds_vs_oracle(gpu, gname, order, bounds, k, rows):
+    p, ix, v = graph(gname)
+    n, d = p.size - 1, 256
+    x = graphs.features(n, d, seed=k)
+    g = graphs.features(n, d, seed=k + 1)
+    od, oi = oracle.maxk(x.numpy(), k)
+    ref_f, mag_f = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    ref_b, mag_b = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k,
+                        options=dict(col_order=order, bwd_chunk_bounds=bounds,
+                                     bwd_row_order=rows, bwd_tasks_per_cu=8,
+                                     bwd_min_task_edges=2000))
+    info = plan.info()
+    assert info["bwd_row_order"] == rows
+    assert info["col_order"] == {"identity": 1, "scattered": 2, "clustered": 3}[order]
+    assert info["bwd_chunk_bounds"] == bounds
+    assert_close(plan.forward(dev(od, gpu), dev(oi, gpu)), ref_f, mag_f)
+    gs = plan.backward(g.to(gpu), dev(oi, gpu))
+    assert_close(gs, ref_b, mag_b)
+    # every element written (the slab flush stores zero blocks too)
+    again = torch.full_like(gs, float("nan"))
+    plan.backward(g.to(gpu), dev(oi, gpu), again)
+    torch.cuda.synchronize()
+    assert not torch.isnan(again).any()
+    assert_close(again, ref_b, mag_b)
+
+
+def test_given_col_order(gpu):
+    p, ix, v = graph("community")
+    n, d, k = p.size - 1, 256, 16
+    g = graphs.features(n, d, seed=3)
+    _, oi = oracle.maxk(graphs.features(n, d, seed=2).numpy(), k)
+    ref, mag = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    perm = torch.from_numpy(np.random.RandomState(5).permutation(n).astype(np.int32)).to(gpu)
+    plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k,
+                        col_order=perm)
+    assert plan.info()["col_order"] == 4
+    assert_close(plan.backward(g.to(gpu), dev(oi, gpu)), ref, mag)
+    got = mk.plan_col_order(plan)
+    assert torch.equal(got, perm)
+    bad = perm.clone()
+    bad[7] = bad[8]                        # not a permutation
+    with pytest.raises(RuntimeError, match="permutation"):
+        mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k, col_order=bad)
+    bad[7] = n                             # out of range
+    with pytest.raises(RuntimeError, match="permutation"):
+        mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k, col_order=bad)
+
+
+def test_clustered_order_recovers_hidden_communities(gpu):
+    """On a community graph under a random relabelling, the clustered order puts each
+    community's columns at neighbouring positions: every column block is mostly one
+    community (the scattered and identity orders mix all of them)."""
+    n, e, c = 30_000, 3_000_000, 9
+    ptr, idx = graphs.community_csr(n, e, communities=c, seed=73, shuffle=True, device=gpu)
+    # community of each relabelled node: replay the generator's permutation
+    gen = torch.Generator(device=gpu)
+    gen.manual_seed(73)
+    deg = graphs.lognormal_degrees(n, e - n, 1.2, gen, gpu)
+    m = int(deg.sum())
+    torch.rand(m, generator=gen, device=gpu, dtype=torch.float64)
+    torch.rand(m, generator=gen, device=gpu)
+    perm = torch.randperm(n, generator=gen, device=gpu)
+    size = -(-n // c)
+    comm = torch.empty(n, dtype=torch.int64, device=gpu)
+    comm[perm] = torch.arange(n, device=gpu) // size
+    val = graphs.sage_mean_values(ptr)
+    purity = {}
+    for order in ("identity", "clustered"):
+        plan = mk.GraphPlan(ptr, idx, val, n, idx.numel(), 256, 16, options=dict(col_order=order))
+        C = plan.info()["bwd_block_cols"]
+        pos = mk.plan_col_order(plan) if order == "clustered" else torch.arange(n, device=gpu)
+        labels = comm[pos.long()]
+        pur = []
+        for b0 in range(0, n, C):
+            lab = labels[b0:b0 + C]
+            pur.append(torch.bincount(lab, minlength=c).max().item() / lab.numel())
+        purity[order] = float(np.mean(pur))
+    assert purity["identity"] < 0.3
+    assert purity["clustered"] > 0.8, purity
+
+
+@pytest.mark.parametrize("chunks", [1, 2, 7])
+@pytest.mark.parametrize("k", [16, 32])
+def test_twopass_row_chunks(gpu, chunks, k):
+    p, ix, v = graph("uniform")
+    n, d = p.size - 1, 256
+    g = graphs.features(n, d, seed=11)
+    _, oi = oracle.maxk(graphs.features(n, d, seed=12).numpy(), k)
+    ref, mag = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k,
+                        options=dict(bwd_algo=3, bwd_tp_chunks=chunks))
+    info = plan.info()
+    assert info["bwd_algo"] == 3 and info["bwd_tp_chunks"] == chunks
+    # the workspace holds the largest chunk's products
+    assert info["bwd_workspace_peak"] <= (ix.size // chunks + np.diff(p).max()) * k * 4
+    assert_close(plan.backward(g.to(gpu), dev(oi, gpu)), ref, mag)
+    v2 = dev(v * np.float32(-0.5), gpu)
+    plan.refresh_values(v2)
+    ref2, mag2 = oracle.sspmm_backward(p, ix, v * np.float32(-0.5), g.numpy(), oi, with_mag=True)
+    assert_close(plan.backward(g.to(gpu), dev(oi, gpu)), ref2, mag2)
+
+
+@pytest.mark.parametrize("k", [16, 32])
+@pytest.mark.parametrize("pattern", ["all_same", "pairs", "one_row"])
+def test_fixed_point_repeated_selectors(gpu, k, pattern):
+    """Rows whose nonzero entries repeat a selector add several terms to one LDS slot. The
+    fixed-point bound must cover the sum (a max |x| bound let k near-maximal terms reach
+    2^52 and wrap the 51-bit residue): forced fixed point against the oracle."""
+    ptr, idx = graphs.synthetic_csr(4000, 200_000, seed=74)
+    p, ix = ptr.numpy(), idx.numpy()
+    v = np.random.RandomState(74).uniform(0.5, 1.0, ix.size).astype(np.float32)
+    n, d = p.size - 1, 256
+    od, oi = oracle.maxk(graphs.features(n, d, seed=75).numpy(), k)
+    od = np.abs(od).astype(np.float32)
+    big = np.float32(1.0 - 2.0 ** -20)
+    if pattern == "all_same":
+        oi[:] = 5
+        od[:] = big
+    elif pattern == "pairs":
+        oi[:, 1::2] = oi[:, 0::2]
+        od[:, :2] = big
+    else:
+        oi[17, :] = 200
+        od[17, :] = big
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k,
+                        options=dict(fwd_fixed=1))
+    assert_close(plan.forward(dev(od, gpu), dev(oi, gpu)), ref, mag)
+
+
+def _stats_numpy(od, oi):
+    """maxk_cbsr_stats restated: per row max |x|, or the sum when nonzero selectors do not
+    strictly ascend; the min nonzero |x|."""
+    a = np.abs(od)
+    mx, mn = 0.0, np.inf
+    for r in range(a.shape[0]):
+        nz = a[r] != 0
+        if not nz.any():
+            continue
+        s = oi[r][nz].astype(np.int64)
+        rep = bool((np.diff(s) <= 0).any())
+        acc = np.float32(0.0)
+        for t in a[r][nz]:                   # the kernel's sequential f32 sum
+            acc = np.float32(acc + np.float32(t))
+        b = np.float32(acc * np.float32(1 + 2.0 ** -10)) if rep else a[r].max()
+        mx = max(mx, float(max(b, a[r].max())))
+        mn = min(mn, float(a[r][nz].min()))
+    return mx, mn
+
+
+def test_cbsr_stats_and_forward_ex_split(gpu):
+    ptr, idx = graphs.synthetic_csr(3000, 90_000, seed=76)
+    p, ix = ptr.numpy(), idx.numpy()
+    v = graphs.sage_mean_values(ptr).numpy()
+    n, d, k = p.size - 1, 256, 16
+    od, oi = oracle.maxk(graphs.features(n, d, seed=77).numpy(), k)
+    od, oi = od.copy(), oi.copy()
+    oi[9, 3] = oi[9, 2]                      # one row with a repeated selector
+    od[10, :] = 0.0                          # an empty row
+    st = mk.cbsr_stats(dev(od, gpu), dev(oi, gpu)).cpu().numpy().view(np.uint32)[0]
+    mx, mn = _stats_numpy(od, oi)
+    assert st[0] == np.float32(mx).view(np.uint32)
+    assert st[1] == 0x7FFFFFFF - np.float32(mn).view(np.uint32)
+    # the stats of two halves of the table, as the multi-GPU path gathers them per rank
+    sd, si = dev(od, gpu), dev(oi, gpu)
+    halves = torch.cat([mk.cbsr_stats(sd[:1500], si[:1500]), mk.cbsr_stats(sd[1500:], si[1500:])])
+    plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k,
+                        options=dict(fwd_fixed=1))
+    a = plan.forward(sd, si)
+    b = plan.forward(sd, si, stats=halves)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    assert_close(b, ref, mag)
+
+
+@pytest.mark.parametrize("width", [30, 66, 7])
+def test_dense_spmm_any_width(gpu, width):
+    ptr, idx = graphs.synthetic_csr(2000, 40_000, seed=78)
+    p, ix = ptr.numpy(), idx.numpy()
+    v = graphs.sage_mean_values(ptr).numpy()
+    x = graphs.features(2000, width, seed=79)
+    ref = oracle.dense_spmm(p, ix, v, x.numpy())
+    mag = oracle.dense_spmm(p, ix, np.abs(v), np.abs(x.numpy()))
+    y = mk.dense_spmm(dev(p, gpu), dev(ix, gpu), dev(v, gpu), x.to(gpu))
+    assert y.shape == (2000, width)
+    assert_close(y, ref, mag, rtol=2e-6 * 64)
+
+
+def test_get_info_v1_writes_only_v1_fields(gpu):
+    p, ix, v = graph("uniform")
+    plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), p.size - 1, ix.size, 256, 16)
+    buf = (ctypes.c_uint8 * ctypes.sizeof(_lib.PlanInfo))(*([0xAB] * ctypes.sizeof(_lib.PlanInfo)))
+    assert _lib.lib.maxk_plan_get_info(plan.handle, ctypes.cast(buf, ctypes.c_void_p)) == 0
+    v1 = _lib.PlanInfo.col_order.offset
+    assert all(b == 0xAB for b in bytes(buf)[v1:])
+    info = _lib.PlanInfo.from_buffer_copy(bytes(buf))
+    assert info.num_edges == ix.size and info.bwd_algo in (1, 2, 3)
+
+
+def test_auto_row_order_follows_dense_runs(gpu):
+    """bwd_row_order auto: scattered rows only where the ascending-row block streams are
+    mostly dense runs (an ID-ordered community graph), ascending elsewhere."""
+    expect = {"uniform": 1, "community": 2, "community_shuffled": 1}
+    for name, want in expect.items():
+        p, ix, v = graph(name)
+        plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), p.size - 1, ix.size, 256, 16)
+        assert plan.info()["bwd_row_order"] == want, name

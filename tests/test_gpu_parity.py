@@ -548,6 +548,31 @@ PLAN_OPTIONS = [
     dict(fwd_fixed=1, quad_loads=1), dict(fwd_fixed=1, fwd_phases=3),
     # two-pass backward with the products stored in column order
     dict(bwd_algo=3, bwd_tp_store=2), dict(bwd_algo=3, bwd_tp_store=1),
+    # ABI 2: chunk bounds (equal edges / equal cost with two pair costs), column orders of
+    # the backward blocks (scattered, clustered) with every packed kernel and flush, two-pass
+    # row chunks
+    dict(bwd_chunk_bounds=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_chunk_bounds=3, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_chunk_bounds=3, bwd_row_cost=400, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_chunk_bounds=3, bwd_row_cost=1, bwd_tasks_per_cu=64, bwd_min_task_edges=16),
+    dict(col_order="scattered"), dict(col_order="clustered"),
+    dict(col_order="scattered", bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(col_order="clustered", bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=1),
+    dict(col_order="scattered", bwd_features_per_lane=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(col_order="scattered", bwd_features_per_lane=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(col_order="clustered", bwd_slot_groups=2, bwd_piece_edges=500),
+    dict(col_order="clustered", bwd_lds_bytes=4096), dict(col_order="scattered", bwd_sel_lds=2),
+    dict(col_order="scattered", bwd_algo=3), dict(col_order="clustered", bwd_algo=2),
+    dict(col_order="clustered", bwd_accumulator="f64"),
+    dict(col_order="identity", bwd_chunk_bounds=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_algo=3, bwd_tp_chunks=2), dict(bwd_algo=3, bwd_tp_chunks=5),
+    dict(bwd_algo=3, bwd_tp_chunks=3, bwd_tp_store=2),
+    # row order inside the block streams (ascending / scattered) with chunks, cost bounds,
+    # slot groups and a column order
+    dict(bwd_row_order=1), dict(bwd_row_order=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_row_order=1, bwd_chunk_bounds=3, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(bwd_row_order=2, col_order="clustered", bwd_slot_groups=2, bwd_piece_edges=500),
+    dict(bwd_row_order=2, bwd_features_per_lane=1, bwd_tasks_per_cu=64, bwd_min_task_edges=16),
 ]
 
 
@@ -599,7 +624,9 @@ def test_plan_options_rejected(gpu):
                 dict(bwd_algo=4), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
                 dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3),
                 dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3), dict(fwd_two_tables=3),
-                dict(bwd_flush=3), dict(bwd_piece_edges=-1), dict(bwd_chunk_bounds=3)):
+                dict(bwd_flush=3), dict(bwd_piece_edges=-1), dict(bwd_chunk_bounds=4),
+                dict(bwd_row_cost=-1), dict(col_order=5), dict(col_order=4),
+                dict(bwd_tp_chunks=-2), dict(bwd_row_order=3)):
         with pytest.raises(RuntimeError):
             mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
 

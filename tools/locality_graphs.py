@@ -1,17 +1,18 @@
 """Supplementary measurement (tooling): the SpGEMM forward and SSpMM backward on
-Reddit-sized graphs with and without column locality.
+Reddit-sized graphs with and without column locality, for a list of plan option sets.
 
   uniform    : graphs.synthetic_csr, the BASELINE workload (uniform random columns)
   community  : graphs.community_csr, 41 communities, p_in 0.76, in ID order (locality visible)
   shuffled   : the same community graph under a random relabelling (locality hidden)
 
-Prints one JSON line per (graph, k): E, fwd/bwd ms (HIP events, median of 5 x 10) and the
-algorithmic-byte roofline fraction of each kernel.
-  python tools/locality_graphs.py [--k 16,32]"""
+Prints one JSON line per (graph, k, option set): E, plan build s, fwd/bwd ms (HIP events,
+median of 5 x 10), the algorithmic-byte roofline fraction of each kernel, and the plan info.
+  python tools/locality_graphs.py [--k 16,32] [--opts '[{}, {"col_order": 3}]']"""
 import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "spgemm-gnn_amd"))
@@ -39,10 +40,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--k", default="16")
     ap.add_argument("--graphs", default="uniform,community,shuffled")
-    ap.add_argument("--opts", default="{}")
+    ap.add_argument("--opts", default="[{}]", help="JSON option dict or list of dicts")
+    ap.add_argument("--which", default="both", choices=["fwd", "bwd", "both"])
+    ap.add_argument("--dataset", default="reddit")
     args = ap.parse_args()
+    opt_sets = json.loads(args.opts)
+    if isinstance(opt_sets, dict):
+        opt_sets = [opt_sets]
     dev = torch.device("cuda:0")
-    n, e0 = graphs.DATASETS["reddit"]
+    n, e0 = graphs.DATASETS[args.dataset]
     d = 256
     h = graphs.features(n, d, seed=97, device=dev)
     g = graphs.features(n, d, seed=98, device=dev)
@@ -55,19 +61,31 @@ def main():
         e = idx.numel()
         for k in [int(x) for x in args.k.split(",")]:
             sd, si = mk.maxk_forward(h, k, return_index=True)
-            plan = mk.GraphPlan(ptr, idx, val, n, e, d, k, options=json.loads(args.opts))
-            out = plan.forward(sd, si)
-            gr = plan.backward(g, si)
-            tf = timeit(lambda: plan.forward(sd, si, out))
-            tb = timeit(lambda: plan.backward(g, si, gr))
-            fb = 4 * (n + 1) + 8 * e + 5 * k * n + 4 * d * n
-            bb = 4 * (n + 1) + 8 * e + 4 * d * n + k * n + 4 * k * n
-            print(json.dumps({"graph": name, "k": k, "num_edges": e, "fwd_ms": round(tf, 4),
-                              "bwd_ms": round(tb, 4), "edges_per_s": 2 * e / ((tf + tb) * 1e-3),
-                              "fwd_roofline_frac": fb / (tf * 1e-3) / 8e12,
-                              "bwd_roofline_frac": bb / (tb * 1e-3) / 8e12,
-                              "info": plan.info()}), flush=True)
-            del plan
+            for opts in opt_sets:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                plan = mk.GraphPlan(ptr, idx, val, n, e, d, k, options=opts)
+                torch.cuda.synchronize()
+                build_s = time.perf_counter() - t0
+                tf = tb = None
+                if args.which in ("fwd", "both"):
+                    out = plan.forward(sd, si)
+                    tf = timeit(lambda: plan.forward(sd, si, out))
+                if args.which in ("bwd", "both"):
+                    gr = plan.backward(g, si)
+                    tb = timeit(lambda: plan.backward(g, si, gr))
+                fb = 4 * (n + 1) + 8 * e + 5 * k * n + 4 * d * n
+                bb = 4 * (n + 1) + 8 * e + 4 * d * n + k * n + 4 * k * n
+                print(json.dumps({
+                    "graph": name, "k": k, "opts": opts, "num_edges": e,
+                    "build_s": round(build_s, 3),
+                    "fwd_ms": None if tf is None else round(tf, 4),
+                    "bwd_ms": None if tb is None else round(tb, 4),
+                    "fwd_roofline_frac": None if tf is None else fb / (tf * 1e-3) / 8e12,
+                    "bwd_roofline_frac": None if tb is None else bb / (tb * 1e-3) / 8e12,
+                    "info": plan.info()}), flush=True)
+                del plan
+            del sd, si
         del ptr, idx, val
 
 
