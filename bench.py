@@ -162,6 +162,9 @@ def main():
                     help="column phases of the N > 1 exchange (all-gather / reduce-scatter of "
                          "one phase overlapping the other's compute; 1 = one-shot, the default: "
                          "2 phases cost +14 %% per-rank compute at W=8, tools/shard_time.py)")
+    ap.add_argument("--split", action="store_true",
+                    help="N > 1: local-columns-first split (own-column edges computed while the "
+                         "all-gather / reduce-scatter are in flight; maxk_kernels.dist)")
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--cpu-sample", type=float, default=1.0,
                     help="fraction of E timed per direction for the CPU baseline")
@@ -243,25 +246,20 @@ def main():
             fwd()
             bwd()
     else:
-        shard = ShardedAggregation(part, rank, ptr, idx, val, d, k)
+        shard = ShardedAggregation(part, rank, ptr, idx, val, d, k, split=args.split)
         # the top-k lands in the shard's padded send buffers: the exchange copies nothing
         sp_data, sp_index = mk.maxk_forward(h, k, return_index=True, out=shard.local_buffers())
         plans = shard.plans
         info = plans[0].info()
         info["num_edges"] = sum(pl.info()["num_edges"] for pl in plans)
-        out = torch.empty((r1 - r0, d), dtype=torch.float32, device=dev)
-        grad_sp = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
+        grad_sp = shard.grad_table
         shard.gather(sp_data, sp_index)
-        nc = part.phase_cols
 
-        def fwd():  # this rank's kernels alone (all phases), no collectives
-            for q, pl in enumerate(plans):
-                pl.forward(shard.table_data[q * nc:(q + 1) * nc],
-                           shard.table_index[q * nc:(q + 1) * nc], out, accumulate=q > 0)
+        def fwd():  # this rank's kernels alone (all parts), no collectives
+            shard.compute_forward()
 
         def bwd():
-            for q, pl in enumerate(plans):
-                pl.backward(g, shard.table_index[q * nc:(q + 1) * nc], grad_sp[q * nc:(q + 1) * nc])
+            shard.compute_backward(g)
 
         def step():
             shard.forward(sp_data, sp_index)
@@ -333,14 +331,21 @@ def main():
     achieved = bwd_gbs if dom == "sspmm_bwd" else fwd_gbs
     traffic = None
     detail = {}
+    lib_sha = mk._lib.lib_sha256()
+    traffic_sha = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             key = f"{tkey}:k{k}:d{d}:n{world}"
+            traffic_sha = tj.get(key, {}).get("lib_sha256")
             traffic = tj.get(key, {}).get(dom)
             detail = tj.get(key, {}).get(dom + "_detail", {})
         except (OSError, ValueError):
             traffic = None
+    # a figure collected on another kernel binary says nothing about this one
+    traffic_stale = traffic is not None and traffic_sha != lib_sha
+    if traffic_stale:
+        traffic, detail = None, {}
 
     result = {
         "metric": METRIC,
@@ -362,7 +367,8 @@ def main():
             "dim_k": k,
             "parallelism": "single-gpu" if world == 1 else
             f"row-partition x{world} + {'RCCL' if backend == 'nccl' else 'gloo (rehearsal)'} "
-            f"all-gather(CBSR) / reduce-scatter(grad_sp)",
+            f"all-gather(CBSR) / reduce-scatter(grad_sp)"
+            + (", local-columns-first split" if args.split else ""),
         },
         "roofline": {
             "bound": "hbm",
@@ -372,6 +378,9 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_stale": traffic_stale,
+            "traffic_lib_sha256": traffic_sha,
+            "lib_sha256": lib_sha,
             "algorithmic_bytes": bb if dom == "sspmm_bwd" else fb,
         },
         "fwd_ms": fwd_ms,
@@ -402,13 +411,16 @@ def main():
     def sweep_traffic(ks, tf, tb):
         """PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE per launch, profiles/pmc_traffic.json) of
         the k's forward and backward kernels, its rate, and its ratio to the algorithmic
-        bytes (traffic well above the compulsory bytes = re-reads)."""
+        bytes (traffic well above the compulsory bytes = re-reads); null when the entry was
+        collected on another kernel binary."""
         ent = {}
         try:
             ent = json.load(open(args.traffic_json)).get(f"{tkey}:k{ks}:d{d}:n1", {})
         except (OSError, ValueError):
             pass
-        out = {}
+        out = {"traffic_stale": bool(ent) and ent.get("lib_sha256") != lib_sha}
+        if out["traffic_stale"]:
+            ent = {}
         for dirn, kern, t, ab in (("fwd", "spgemm_fwd", tf, fwd_bytes(n, e, ks, d)),
                                   ("bwd", "sspmm_bwd", tb, bwd_bytes(n, e, ks, d))):
             tr = ent.get(kern)

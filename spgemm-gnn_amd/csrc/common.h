@@ -51,7 +51,9 @@ constexpr double kBwdTwoPassReuse = 0.75;
 constexpr int kBwdRowsPerWave = 4;  // row pass: most destination rows one wavefront stages
 // two-pass backward: the E x k product workspace is cut into row chunks of at most this many
 // bytes (one row pass + one column pass per chunk; bwd_tp_chunks overrides)
-constexpr double kBwdTwoPassWorkspaceCap = 4.0 * (1ull << 30);
+// (ogbn-products k = 32, 15.8 GB in one chunk: 1 / 2 / 4 / 8 chunks ran 8.11 / 8.68 / 10.49 /
+// 14.60 ms; every chunk's column pass visits every column)
+constexpr double kBwdTwoPassWorkspaceCap = 16.0 * (1ull << 30);
 // cost-balanced backward chunks: a (column block, destination row) pair costs this many
 // quarter-edges on top of its edges (its grad_out lines are fetched once per pair). Measured
 // on the Reddit-size 41-community graph in ID order (ascending rows), k = 16: 1, 4, 8, 16, 24

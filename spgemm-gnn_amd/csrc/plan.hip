@@ -1449,11 +1449,12 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     // every chunk task clears and flushes its whole block (C * k floats) however few edges
     // it has: keep >= kBwdMinTaskEdges edges per task (a row shard of a multi-GPU partition
     // has 1/W of the edges over the same blocks)
-    // ... but not fewer tasks than CUs while those keep >= 16k edges (a row shard of an
-    // 8-GPU partition: 256 tasks of ~56k edges ran 0.24 ms, 512 of ~28k 0.27, 128 0.40)
+    // ... but not fewer tasks than CUs while those keep >= 4k edges (a row shard of an
+    // 8-GPU partition: 256 tasks of ~56k edges ran 0.24 ms, 512 of ~28k 0.27, 128 0.40; the
+    // own-column part of such a shard, 1.8 M edges over 16 blocks: 16 tasks ran 0.35 ms)
     int64_t nch64 = std::min<int64_t>(chunks, E / ((int64_t)nblocks * min_task_edges));
     const int64_t fl = ((int64_t)cus + (int64_t)nblocks * S - 1) / ((int64_t)nblocks * S);
-    if (o.bwd_min_task_edges == 0 && nch64 < fl && E / ((int64_t)nblocks * fl) >= 16384)
+    if (o.bwd_min_task_edges == 0 && nch64 < fl && E / ((int64_t)nblocks * fl) >= 4096)
       nch64 = std::min<int64_t>(chunks, fl);
     nch64 = std::max<int64_t>(1, nch64);
     // One 512-thread work-group per CU: a task count just past a multiple of the CUs leaves
@@ -1535,7 +1536,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       // column locality (an ID-ordered community) a block's stream is a dense run of
       // community rows (~100 edges per pair) between long sparse stretches (~1 edge per pair),
       // and equal-edge chunks of it differ several-fold in time. Each block gets chunks in
-      // proportion to its cost (nch on average), each chunk an equal share of that cost.
+      // proportion to its cost (at least nch on average), each chunk an equal share of it.
       const int rc4 = o.bwd_row_cost ? o.bwd_row_cost : kBwdRowCost4;
       CH_TRY(hipMalloc(&d_cum, sizeof(int64_t) * E));
       hipLaunchKernelGGL(bwd_cost_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, keys_out,
@@ -1557,7 +1558,12 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       std::vector<int32_t> nchb(nblocks);
       for (int b = 0; b < nblocks; ++b) {
         const int64_t T = bc[b + 1] - bc[b], nnz = offs[b + 1] - offs[b];
-        int64_t c = std::max<int64_t>(1, std::llround((double)T / tau));
+        // rounded, but no task above 1.25 tau: one work-group per CU runs the tasks in rounds,
+        // so a task count past a multiple of the CUs costs a round (ceil everywhere: Reddit
+        // k = 16 tasks 512 -> ~560), and a block of ~1.5 tau in one chunk stretches one
+        // (rounding alone: an 8-GPU row shard, ~2 chunks per block, 0.244 -> 0.303 ms)
+        int64_t c = std::max<int64_t>({(int64_t)1, (int64_t)std::llround((double)T / tau),
+                                       (int64_t)std::ceil((double)T / (1.25 * tau) - 1e-9)});
         c = std::min<int64_t>(c, std::max<int64_t>(1, std::min<int64_t>(nnz, 64ll * nch)));
         nchb[b] = (int32_t)c;
         for (int64_t j = 1; j < c; ++j) {

@@ -133,6 +133,97 @@ __device__ __forceinline__ double fwd_fix_scale(int2 fix, const uint32_t* xs, in
   return __builtin_ldexp(1.0, sc);
 }
 
+// cbsr_stats_kernel for k % 4 == 0 (k <= 256): L = k/4 lanes per row, each loading its 4
+// values (float4) and their 4 selectors (one dword), rows 64/L per wave, coalesced. Per row,
+// inclusive prefix scans over its L lanes (shuffles) give the sum of |x|, the max |x|, and
+// whether a lane's first nonzero selector is <= the last nonzero selector of any earlier lane
+// (or its own nonzero selectors do not ascend): the same bound as the thread-per-row kernel
+// below, with the row sum added in another order (its 2^-10 headroom covers that).
+__global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restrict__ x,
+                                                          const uint8_t* __restrict__ sel,
+                                                          int64_t nrows, int k, uint32_t* st0,
+                                                          uint32_t* st1) {
+  __shared__ uint32_t smx[256 / kWave], smn[256 / kWave];
+  const int L = k >> 2;
+  const int RW = kWave / L;  // rows per wave
+  const int lane = threadIdx.x & (kWave - 1);
+  const int slot = lane / L, q = lane - slot * L;
+  const bool on = slot < RW;
+  uint32_t mx = 0u, mn = 0x7fffffffu;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+  for (int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) * RW;
+       r0 < nrows; r0 += waves * RW) {
+    const int64_t r = r0 + slot;
+    const bool live = on && r < nrows;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t s = 0u;
+    if (live) {
+      v = *reinterpret_cast<const float4*>(x + r * k + 4 * q);
+      s = *reinterpret_cast<const uint32_t*>(sel + r * k + 4 * q);
+    }
+    const uint32_t b[4] = {__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu,
+                           __float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu};
+    uint32_t lmax = 0u, lmin = 0x7fffffffu;
+    float lsum = 0.f;
+    int first = -1, last = -1;
+    bool rep = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (b[i] == 0u) continue;
+      const int si = (int)((s >> (8 * i)) & 0xffu);
+      lmax = max(lmax, b[i]);
+      lmin = min(lmin, b[i]);
+      lsum += __uint_as_float(b[i]);
+      rep = rep || si <= last;
+      if (first < 0) first = si;
+      last = si;
+    }
+    // inclusive prefix over the row's lanes: sum, max, repeat flag, max of last selectors
+    int pl = last;  // max nonzero selector of lanes <= q
+    for (int d = 1; d < L; d <<= 1) {
+      const float os = __shfl(lsum, lane - d);
+      const uint32_t om = (uint32_t)__shfl((int)lmax, lane - d);
+      const int orp = __shfl((int)rep, lane - d);
+      const int opl = __shfl(pl, lane - d);
+      if (q >= d) {
+        lsum += os;
+        lmax = max(lmax, om);
+        rep = rep || orp;
+        pl = max(pl, opl);
+      }
+    }
+    const int prev = __shfl(pl, lane - 1);  // max nonzero selector of lanes < q
+    const bool cross = q > 0 && first >= 0 && first <= prev;
+    // the row's repeat flag = OR over its lanes (prefix OR, taken at the last lane)
+    int any = cross ? 1 : 0;
+    for (int d = 1; d < L; d <<= 1) {
+      const int o = __shfl(any, lane - d);
+      if (q >= d) any |= o;
+    }
+    if (live) {
+      mn = min(mn, lmin);
+      if (q == L - 1) {
+        const bool rrep = rep || any;
+        const uint32_t rb =
+            rrep ? max(lmax, __float_as_uint(lsum * (1.0f + 0x1p-10f)) & 0x7fffffffu) : lmax;
+        mx = max(mx, rb);
+      }
+    }
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+  }
+  const int w = threadIdx.x / kWave;
+  if (lane == 0) { smx[w] = mx; smn[w] = mn; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 256 / kWave; ++i) { mx = max(mx, smx[i]); mn = min(mn, smn[i]); }
+    atomicMax(st0, mx);
+    atomicMax(st1, 0x7fffffffu - mn);
+  }
+}
+
 // Statistics of a CBSR table for fwd_fix_scale, one thread per row (bit patterns of
 // non-negative floats order like integers): *st0 = max over rows of the row's slot bound B,
 // *st1 = 0x7fffffff - min nonzero |x|. B is max |x| when the row's nonzero entries have
@@ -388,12 +479,14 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   t.e0 = phase_off[ti * (phases + 1) + phase];
   t.e1 = phase_off[ti * (phases + 1) + phase + 1];
   }
-  if ((phase > 0 || accum) && t.e0 == t.e1) continue;  // nothing to add (uniform)
-  // fixed-point accumulation for this task (LdsFix), else f64; the 8-byte slots are the same
+  const bool cont = phase > 0 || accum;  // rows of out hold a prior sum to add to
+  if (cont && t.e0 == t.e1) continue;  // nothing to add (uniform)
+  // fixed-point accumulation for this task (LdsFix), else f64; the 8-byte slots are the same.
+  // A continuing launch in fixed point sums its own terms from zero and adds the prior f32
+  // row at the write-back (one more f32 rounding, as a column phase of the reference would)
   double fsc = 0.0;
   if constexpr (VEC == 4 && ACC == MAXK_ACC_F64) {
-    if (fix_tab && !(phase > 0 || accum))
-      fsc = fwd_fix_scale(fix_tab[ti], xstat, xs_n, xs_stride, xs_off2);
+    if (fix_tab) fsc = fwd_fix_scale(fix_tab[ti], xstat, xs_n, xs_stride, xs_off2);
   }
   const bool fixed = fsc != 0.0;
   unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(smem_d);
@@ -402,7 +495,7 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   const int n = nrows * D;
   const int DS = D + kFwdRowPad;  // LDS row stride (elements)
   __syncthreads();  // the previous task's write-back has finished reading acc
-  if ((phase > 0 || accum) && !split) {  // continue from the stored rows
+  if (cont && !split && !fixed) {  // continue from the stored rows
     const float* src = out + (size_t)t.row0 * D;
     for (int i = threadIdx.x; i < n; i += NT) {
       const int r = i / D;
@@ -471,11 +564,18 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     return (float)acc[r * DS + (i - r * D)];
   };
   if (!split) {
+    const bool add = cont && fixed;  // the prior row is added here (see above)
     if ((D & 3) == 0) {
-      for (int i = threadIdx.x * 4; i < n; i += NT * 4)
-        *reinterpret_cast<float4*>(dst + i) = make_float4(get(i), get(i + 1), get(i + 2), get(i + 3));
+      for (int i = threadIdx.x * 4; i < n; i += NT * 4) {
+        float4 v = make_float4(get(i), get(i + 1), get(i + 2), get(i + 3));
+        if (add) {
+          const float4 o = *reinterpret_cast<const float4*>(dst + i);
+          v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+        }
+        *reinterpret_cast<float4*>(dst + i) = v;
+      }
     } else {
-      for (int i = threadIdx.x; i < n; i += NT) dst[i] = get(i);
+      for (int i = threadIdx.x; i < n; i += NT) dst[i] = add ? dst[i] + get(i) : get(i);
     }
   } else {
     for (int i = threadIdx.x; i < D; i += NT) global_add(dst + i, get(i));
@@ -1359,6 +1459,26 @@ static hipError_t allow_lds(K* kernel, size_t bytes) {
 
 using namespace maxk;
 
+// Fixed-point statistics of a CBSR table into two zeroed words: the lane-parallel kernel
+// for k % 4 == 0 (~10 us for Reddit at k = 16), one thread per row otherwise.
+static int launch_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int64_t nrows, int k,
+                             uint32_t* st0, uint32_t* st1, int cus, hipStream_t s) {
+  if (nrows <= 0) return MAXK_OK;
+  if (k % 4 == 0) {
+    const int64_t rows_per_block = (256 / kWave) * (kWave / (k / 4));
+    const int grid = (int)std::max<int64_t>(
+        1, std::min<int64_t>((nrows + rows_per_block - 1) / rows_per_block, 4 * cus));
+    hipLaunchKernelGGL(cbsr_stats4_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nrows,
+                       k, st0, st1);
+  } else {
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nrows + 255) / 256, 2 * cus));
+    hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nrows,
+                       k, st0, st1);
+  }
+  MAXK_LAUNCH_CHECK("cbsr_stats launch");
+  return MAXK_OK;
+}
+
 static int check_plan(const maxk_plan* plan, const int32_t* ptr, const int32_t* idx,
                       int32_t N, int64_t E, int32_t k, int32_t D, const char* who) {
   MAXK_CHECK_ARG(plan != nullptr, std::string(who) + ": plan is null");
@@ -1374,10 +1494,14 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
                                const float* val, const float* sp_data, const uint8_t* sp_index,
                                float* out, int32_t N, int64_t E, int32_t k, int32_t D,
                                void* stream, int accum, void* ws, int64_t ws_bytes,
-                               const uint32_t* stats = nullptr, int n_stats = 0) {
+                               const uint32_t* stats = nullptr, int n_stats = 0,
+                               int64_t stats_stride = 2) {
   MAXK_CHECK_ARG(N >= 0 && E >= 0, "maxk_spgemm_forward: negative size");
   MAXK_CHECK_ARG(stats == nullptr || (n_stats >= 1 && n_stats <= 1024),
                  "maxk_spgemm_forward_ex: n_stats must be in [1, 1024]");
+  if (stats_stride == 0) stats_stride = 2;
+  MAXK_CHECK_ARG(stats_stride >= 2 && stats_stride * (int64_t)n_stats < (int64_t)INT32_MAX,
+                 "maxk_spgemm_forward_ex: stats_stride must be >= 2 (or 0)");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_spgemm_forward: dim_origin must be in [1, 256]");
   MAXK_CHECK_ARG(k >= 1 && k <= D, "k must be between 1 and input dimension");
   int rc = check_plan(plan, ptr, idx, N, E, k, D, "maxk_spgemm_forward");
@@ -1431,21 +1555,19 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   const int2* fix_tab = nullptr;
   const uint32_t* xstat = nullptr;
   int xs_n = 1, xs_stride = 0, xs_off2 = 32;
-  if (plan->fwd_fix && !accum && plan->num_cols > 0) {
+  if (plan->fwd_fix && plan->num_cols > 0) {
     fix_tab = plan->fwd_fix;
     if (stats) {
       xstat = stats;
       xs_n = n_stats;
-      xs_stride = 2;
+      xs_stride = (int)stats_stride;
       xs_off2 = 1;
     } else {
       uint32_t* st = reinterpret_cast<uint32_t*>(ws_base + plan->fwd_xstat_off);
       MAXK_HIP_TRY(hipMemsetAsync(st, 0, 256, s));
-      const int64_t nr = plan->num_cols;
-      const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nr + 255) / 256, 2 * plan->cus));
-      hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nr, k,
-                         st, st + 32);
-      MAXK_LAUNCH_CHECK("cbsr_stats launch");
+      const int rc = launch_cbsr_stats(sp_data, sp_index, plan->num_cols, k, st, st + 32,
+                                       plan->cus, s);
+      if (rc) return rc;
       xstat = st;
     }
   }
@@ -1562,12 +1684,13 @@ extern "C" int maxk_spgemm_forward_ex(const maxk_plan* plan, const int32_t* ptr,
                                       const float* sp_data, const uint8_t* sp_index, float* out,
                                       int32_t N, int64_t E, int32_t k, int32_t D,
                                       int32_t accumulate, const uint32_t* stats,
-                                      int32_t n_stats, void* workspace,
+                                      int32_t n_stats, int64_t stats_stride, void* workspace,
                                       int64_t workspace_bytes, void* stream) {
   MAXK_CHECK_ARG(accumulate == 0 || accumulate == 1,
                  "maxk_spgemm_forward_ex: accumulate must be 0 or 1");
   return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream,
-                             accumulate, workspace, workspace_bytes, stats, n_stats);
+                             accumulate, workspace, workspace_bytes, stats, n_stats,
+                             stats_stride);
 }
 
 extern "C" int maxk_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int32_t num_rows,
@@ -1584,11 +1707,7 @@ extern "C" int maxk_cbsr_stats(const float* sp_data, const uint8_t* sp_index, in
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((num_rows + 255) / 256, 2 * cus));
-  hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
-                     (int64_t)num_rows, dim_k, stats, stats + 1);
-  MAXK_LAUNCH_CHECK("maxk_cbsr_stats launch");
-  return MAXK_OK;
+  return launch_cbsr_stats(sp_data, sp_index, num_rows, dim_k, stats, stats + 1, cus, s);
 }
 
 extern "C" int maxk_spgemm_forward_acc(const maxk_plan* plan, const int32_t* ptr,

@@ -40,7 +40,8 @@ SIGNATURES = {
     "maxk_plan_get_col_order": (ctypes.c_int, [_vp, _vp, _vp]),
     "maxk_cbsr_stats": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp]),
     "maxk_spgemm_forward_ex": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
-                                              _i32, _i32, _i32, _vp, _i32, _vp, _i64, _vp]),
+                                              _i32, _i32, _i32, _vp, _i32, _i64, _vp, _i64,
+                                              _vp]),
     "maxk_plan_destroy": (ctypes.c_int, [_vp]),
     "maxk_spgemm_forward": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
                                            _i32, _i32, _vp]),
@@ -158,6 +159,17 @@ def _load():
 
 
 lib = _load()
+
+
+def lib_sha256(path: str = LIB_PATH) -> str:
+    """sha256 of the loaded libmaxk_hip.so: ties a measurement (profiles/pmc_traffic.json)
+    to the kernel binary it was taken on."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
 
 
 class MaxKError(RuntimeError):

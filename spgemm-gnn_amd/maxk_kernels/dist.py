@@ -15,6 +15,18 @@ exchange per direction:
 * backward: the local SSpMM produces a partial grad_sp for every (padded) column; an
   RCCL reduce-scatter (sum) returns each rank its own rows' gradient.
 
+Fixed-point statistics: with one phase, every rank's block of the table ends in a spare row.
+Before the all-gather the rank writes the fixed-point statistics of its own rows into the
+selector bytes of that row (``maxk_cbsr_stats``: two words; the value row stays zero, so the
+row adds nothing anywhere), the gathered index table carries one pair per rank and the
+forward reads those W pairs (``maxk_spgemm_forward_ex``) instead of scanning the whole table.
+
+Local-columns-first split (``split=True``, one phase): the rank's edges are cut into those
+whose column it owns and the rest, with a plan each. The forward runs the local plan on the
+send buffers while the all-gather is in flight, then the remote plan accumulates on the
+gathered table. The backward runs the remote plan, starts the reduce-scatter, runs the local
+plan while it is in flight, and adds the local gradient to the scattered one.
+
 Column phases (``phases`` P > 1): every rank's rows are cut into P parts and the table is
 laid out phase-major (phase p holds part p of every rank), so each phase is one all-gather
 and one reduce-scatter of its own. The rank keeps one plan per phase (its edges split by the
@@ -35,9 +47,11 @@ import torch.distributed as dist
 
 class RowPartition:
     """Contiguous destination-row ranges with ~equal nnz per rank, and the phase-major
-    layout of the all-gathered CBSR table (``phases`` parts per rank)."""
+    layout of the all-gathered CBSR table (``phases`` parts per rank; with one phase each
+    rank's block ends in a spare row that carries its fixed-point statistics)."""
 
-    def __init__(self, ptr: torch.Tensor, world_size: int, phases: int = 1):
+    def __init__(self, ptr: torch.Tensor, world_size: int, phases: int = 1,
+                 stats_row: Optional[bool] = None):
         p = ptr.detach().to("cpu", torch.int64)
         n = p.numel() - 1
         e = int(p[-1])
@@ -53,17 +67,21 @@ class RowPartition:
         counts = b[1:] - b[:-1]
         self.max_rows = max(1, int(counts.max()))
         self.phases = max(1, int(phases))
-        self.phase_rows = -(-self.max_rows // self.phases)   # rows of a rank in one phase
-        self.phase_cols = w * self.phase_rows                 # table rows of one phase
-        self.send_rows = self.phases * self.phase_rows        # >= max_rows
+        self.stats_row = (self.phases == 1) if stats_row is None else bool(stats_row)
+        if self.stats_row and self.phases != 1:
+            raise ValueError("the statistics row needs a one-phase partition")
+        self.rows_per_phase = -(-self.max_rows // self.phases)  # node rows of a rank per phase
+        self.phase_rows = self.rows_per_phase + (1 if self.stats_row else 0)
+        self.phase_cols = w * self.phase_rows                  # table rows of one phase
+        self.send_rows = self.phases * self.phase_rows         # >= max_rows
         self.padded_rows = self.phases * self.phase_cols
 
     def rows(self, rank: int):
         return int(self.bounds[rank]), int(self.bounds[rank + 1])
 
     def _position(self, q: torch.Tensor, off: torch.Tensor) -> torch.Tensor:
-        ph = off // self.phase_rows
-        return ph * self.phase_cols + q * self.phase_rows + (off - ph * self.phase_rows)
+        ph = off // self.rows_per_phase
+        return ph * self.phase_cols + q * self.phase_rows + (off - ph * self.rows_per_phase)
 
     def remap_columns(self, idx: torch.Tensor) -> torch.Tensor:
         """Global column id -> position in the padded (phase-major) all-gather table."""
@@ -78,6 +96,10 @@ class RowPartition:
         off = torch.arange(b - a, dtype=torch.int64, device=device)
         return self._position(torch.full_like(off, rank), off)
 
+    def stats_position(self, rank: int) -> int:
+        """Table row of rank's statistics pair (one-phase partitions)."""
+        return rank * self.phase_rows + self.rows_per_phase
+
     def local_csr(self, ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, rank: int):
         """(ptr, remapped idx, val) of rank's rows; ptr rebased to 0."""
         r0, r1 = self.rows(rank)
@@ -91,20 +113,26 @@ class RowPartition:
         """The edges of a local CSR (remapped columns) whose column lies in ``phase``, with
         columns rebased to that phase's table block [0, phase_cols)."""
         lo = phase * self.phase_cols
-        keep = (lidx >= lo) & (lidx < lo + self.phase_cols)
-        n = lptr.numel() - 1
-        rows = torch.repeat_interleave(torch.arange(n, device=lptr.device),
-                                       (lptr[1:] - lptr[:-1]).to(torch.int64))
-        cnt = torch.bincount(rows[keep], minlength=n)
-        pptr = torch.zeros(n + 1, dtype=torch.int64, device=lptr.device)
-        pptr[1:] = torch.cumsum(cnt, 0)
-        return (pptr.to(torch.int32).contiguous(), (lidx[keep] - lo).to(torch.int32).contiguous(),
-                lval[keep].contiguous())
+        return select_csr(lptr, lidx, lval, (lidx >= lo) & (lidx < lo + self.phase_cols), lo)
 
 
-# injected per-phase compute (CPU tests): fwd(phase, table_data_p, table_index_p, out) -> out
-# (out is None for phase 0, else the output to accumulate into); bwd(phase, grad_out,
-# table_index_p) -> grad for the phase's table block
+def select_csr(lptr: torch.Tensor, lidx: torch.Tensor, lval: torch.Tensor,
+               keep: torch.Tensor, shift: int = 0):
+    """The edges of a CSR where ``keep`` holds (row order kept), columns minus ``shift``."""
+    n = lptr.numel() - 1
+    rows = torch.repeat_interleave(torch.arange(n, device=lptr.device),
+                                   (lptr[1:] - lptr[:-1]).to(torch.int64))
+    cnt = torch.bincount(rows[keep], minlength=n)
+    pptr = torch.zeros(n + 1, dtype=torch.int64, device=lptr.device)
+    pptr[1:] = torch.cumsum(cnt, 0)
+    return (pptr.to(torch.int32).contiguous(), (lidx[keep] - shift).to(torch.int32).contiguous(),
+            lval[keep].contiguous())
+
+
+# injected per-part compute (CPU tests): fwd(part, table_data, table_index, out) -> out (out
+# is None for the first part, else the output to accumulate into); bwd(part, grad_out,
+# table_index) -> the part's grad rows. A part reads the table given by ShardedAggregation
+# (its phase's block, or for the split: the send buffers / the whole table).
 FwdFn = Callable[[int, torch.Tensor, torch.Tensor, Optional[torch.Tensor]], torch.Tensor]
 BwdFn = Callable[[int, torch.Tensor, torch.Tensor], torch.Tensor]
 
@@ -113,15 +141,17 @@ class ShardedAggregation:
     """One rank's share of Y = A densify(sp) and of its SSpMM backward.
 
     ``fwd``/``bwd`` default to the gfx950 kernels through one rectangular GraphPlan per
-    column phase (``plan_options``: the same knobs as ``GraphPlan(options=...)``, e.g.
+    part (``plan_options``: the same knobs as ``GraphPlan(options=...)``, e.g.
     ``{"bwd_algo": 3}``); tests on CPU (gloo) inject checker callables to exercise the
-    partition, the phase layout and the collectives.
+    partition, the layouts and the collectives. ``parts[i]`` = (ptr, idx, val, num_cols) of
+    part i: the column phases, or (split) the own-column and the remote-column edges.
     """
 
     def __init__(self, part: RowPartition, rank: int, ptr: torch.Tensor, idx: torch.Tensor,
                  val: torch.Tensor, dim_origin: int, dim_k: int,
                  group: Optional[dist.ProcessGroup] = None, fwd: Optional[FwdFn] = None,
-                 bwd: Optional[BwdFn] = None, plan_options: Optional[dict] = None):
+                 bwd: Optional[BwdFn] = None, plan_options: Optional[dict] = None,
+                 split: bool = False):
         self.part, self.rank, self.group = part, rank, group
         self.dim_origin, self.dim_k = int(dim_origin), int(dim_k)
         self.r0, self.r1 = part.rows(rank)
@@ -129,6 +159,9 @@ class ShardedAggregation:
         self.ptr, self.idx, self.val = part.local_csr(ptr, idx, val, rank)
         dev = self.ptr.device
         P, k = part.phases, self.dim_k
+        if split and P != 1:
+            raise ValueError("the local-columns-first split needs a one-phase partition")
+        self.split = bool(split)
         # padded send buffers (rows >= n_local stay zero) and the all-gathered tables
         self.send_data = torch.zeros((part.send_rows, k), dtype=torch.float32, device=dev)
         self.send_index = torch.zeros((part.send_rows, k), dtype=torch.uint8, device=dev)
@@ -136,22 +169,52 @@ class ShardedAggregation:
         self.table_index = torch.empty((part.padded_rows, k), dtype=torch.uint8, device=dev)
         self.grad_table = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
         self.grad_local = torch.empty((part.send_rows, k), dtype=torch.float32, device=dev)
+        if self.split:
+            lo = rank * part.phase_rows
+            own = (self.idx >= lo) & (self.idx < lo + self.n_local)
+            self.parts = [select_csr(self.ptr, self.idx, self.val, own, lo) + (max(1, self.n_local),),
+                          select_csr(self.ptr, self.idx, self.val, ~own) + (part.padded_rows,)]
+            self.grad_own = torch.empty((max(1, self.n_local), k), dtype=torch.float32, device=dev)
+        else:
+            self.parts = [part.phase_csr(self.ptr, self.idx, self.val, p) + (part.phase_cols,)
+                          for p in range(P)]
         self.plans: List = []
-        if fwd is None or bwd is None:
+        native = fwd is None or bwd is None
+        if native:
             from .ops import GraphPlan
-            for p in range(P):
-                pp, pi, pv = part.phase_csr(self.ptr, self.idx, self.val, p)
+            for pp, pi, pv, nc in self.parts:
                 self.plans.append(GraphPlan(pp, pi, pv, self.n_local, pi.numel(),
-                                            self.dim_origin, self.dim_k,
-                                            num_cols=part.phase_cols, options=plan_options))
-        self._fwd = fwd or (lambda p, d, i, out: self.plans[p].forward(
-            d, i, out, accumulate=out is not None))
-        self._bwd = bwd or (lambda p, g, i: self.plans[p].backward(
-            g, i, self._slice(self.grad_table, p)))
+                                            self.dim_origin, self.dim_k, num_cols=nc,
+                                            options=plan_options))
+        # the statistics pair in the selector bytes of the send buffer's spare row (one
+        # phase, native kernels; 4-byte aligned words: k % 4 == 0, k >= 8)
+        self.stats = native and part.stats_row and k % 4 == 0 and k >= 8
+        rp = part.rows_per_phase
+        self._stats_local = (self._words(self.send_index, rp), 1, 2) if self.stats else None
+        self._stats_all = ((self._words(self.table_index, rp), part.world_size,
+                            part.phase_rows * k // 4) if self.stats else None)
+        self._fwd = fwd or self._native_fwd
+        self._bwd = bwd or (lambda i, g, ti: self.plans[i].backward(g, ti, self._grad_dst(i)))
+
+    @staticmethod
+    def _words(index_table: torch.Tensor, row: int) -> torch.Tensor:
+        """int32 view of a u8 table from ``row`` on (the statistics words of a spare row)."""
+        return index_table[row:].view(-1).view(torch.int32)
+
+    def _native_fwd(self, i, td, ti, out):
+        stats = None
+        if self.stats:
+            stats = self._stats_local if (self.split and i == 0) else self._stats_all
+        return self.plans[i].forward(td, ti, out, accumulate=out is not None, stats=stats)
+
+    def _grad_dst(self, i):
+        if self.split:
+            return self.grad_own if i == 0 else self.grad_table
+        return self._slice(self.grad_table, i)
 
     @property
     def plan(self):
-        """The plan of a one-phase partition (bench.py's per-kernel timing)."""
+        """The plan of a one-part partition (bench.py's per-kernel timing)."""
         return self.plans[0] if len(self.plans) == 1 else None
 
     def _slice(self, table: torch.Tensor, p: int) -> torch.Tensor:
@@ -173,6 +236,15 @@ class ShardedAggregation:
             self.send_data[:n].copy_(sp_data_local)
         if sp_index_local.data_ptr() != self.send_index.data_ptr():
             self.send_index[:n].copy_(sp_index_local)
+        if self.stats:  # this rank's pair, all-gathered with its rows
+            from .ops import cbsr_stats
+            cbsr_stats(self.send_data[:n], self.send_index[:n],
+                       out=self.stats_words(self.send_index, self.part.rows_per_phase))
+
+    @staticmethod
+    def stats_words(index_table: torch.Tensor, row: int) -> torch.Tensor:
+        """The 2 int32 statistics words in the selector bytes of a spare row."""
+        return index_table[row].view(torch.int32)[:2]
 
     def _gather_phase(self, p: int, async_op: bool):
         w1 = dist.all_gather_into_tensor(self._slice(self.table_data, p),
@@ -193,6 +265,13 @@ class ShardedAggregation:
         self._stage(sp_data_local, sp_index_local)
         P = self.part.phases
         works = [self._gather_phase(p, async_op=True) for p in range(P)]
+        if self.split:
+            # own columns from the send buffers while the exchange is in flight
+            out = self._fwd(0, self.send_data[: self.n_local], self.send_index[: self.n_local],
+                            None)
+            for wk in works[0]:
+                wk.wait()
+            return self._fwd(1, self.table_data, self.table_index, out)
         out = None
         for p in range(P):
             for wk in works[p]:
@@ -201,8 +280,30 @@ class ShardedAggregation:
                             out)
         return out
 
+    def compute_forward(self) -> torch.Tensor:
+        """The forward's kernels alone on the current tables (no exchange): per-rank timing."""
+        if self.split:
+            out = self._fwd(0, self.send_data[: self.n_local], self.send_index[: self.n_local],
+                            None)
+            return self._fwd(1, self.table_data, self.table_index, out)
+        out = None
+        for p in range(self.part.phases):
+            out = self._fwd(p, self._slice(self.table_data, p), self._slice(self.table_index, p),
+                            out)
+        return out
+
     def backward(self, grad_out_local: torch.Tensor) -> torch.Tensor:
         g = grad_out_local.contiguous()
+        if self.split:
+            # remote columns first; the own columns' gradient stays here and is computed
+            # while the reduce-scatter is in flight (its slot in the scatter holds zeros)
+            gp = self._bwd(1, g, self.table_index)
+            wk = dist.reduce_scatter_tensor(self.grad_local, gp, op=dist.ReduceOp.SUM,
+                                            group=self.group, async_op=True)
+            gl = self._bwd(0, g, self.send_index[: self.n_local])
+            wk.wait()
+            self.grad_local[: self.n_local].add_(gl[: self.n_local])
+            return self.grad_local[: self.n_local]
         works = []
         for p in range(self.part.phases):
             gp = self._bwd(p, g, self._slice(self.table_index, p))
@@ -212,6 +313,16 @@ class ShardedAggregation:
         for wk in works:
             wk.wait()
         return self.grad_local[: self.n_local]
+
+    def compute_backward(self, grad_out_local: torch.Tensor) -> None:
+        """The backward's kernels alone (no exchange): per-rank timing."""
+        g = grad_out_local.contiguous()
+        if self.split:
+            self._bwd(1, g, self.table_index)
+            self._bwd(0, g, self.send_index[: self.n_local])
+            return
+        for p in range(self.part.phases):
+            self._bwd(p, g, self._slice(self.table_index, p))
 
     def unpad_table(self, table: torch.Tensor) -> torch.Tensor:
         """Padded phase-major table -> natural node order [N, ...] (tests/inspection)."""

@@ -214,11 +214,13 @@ class GraphPlan:
                     f"{{'bwd_algo': 1}} (column blocks) needs less") from exc
 
     def forward(self, sp_data, sp_index, out=None, accumulate: bool = False,
-                stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+                stats=None) -> torch.Tensor:
         """SpGEMM with this plan: sp tables [num_cols, k] -> out [num_rows, D];
         ``accumulate=True`` adds into the given ``out`` instead of overwriting it. ``stats``:
-        int32 [n, 2] fixed-point statistics covering the table (:func:`cbsr_stats` per
-        part; the multi-GPU path gathers one pair per rank) instead of a pass over it."""
+        fixed-point statistics covering the table instead of a pass over it, either an int32
+        [n, 2] tensor of :func:`cbsr_stats` pairs or ``(tensor, n, stride)`` with pair i at
+        32-bit word i * stride of the tensor's storage (the multi-GPU path keeps one pair
+        per rank in a spare row of the gathered table)."""
         ptr, idx, val = self._refs
         if out is None:
             if accumulate:
@@ -228,15 +230,21 @@ class GraphPlan:
         stream = torch.cuda.current_stream(self.device)
         self._begin(stream)
         ws, wsb = self._workspace(self.fwd_ws_bytes)
-        if stats is not None:
+        st, n_st, stride = None, 0, 2
+        if isinstance(stats, tuple):
+            st, n_st, stride = stats
+            _need(st.is_cuda and st.element_size() == 4 and
+                  (n_st - 1) * stride + 2 <= st.numel(), "stats does not hold n pairs")
+        elif stats is not None:
             _need(stats.is_cuda and stats.is_contiguous() and stats.dtype == torch.int32 and
                   stats.dim() == 2 and stats.shape[1] == 2 and stats.shape[0] >= 1,
                   "stats must be a contiguous int32 [n, 2] CUDA tensor")
+            st, n_st = stats, stats.shape[0]
         check(lib.maxk_spgemm_forward_ex(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
                                          _p(sp_index), _p(out), self.num_rows, self.num_edges,
-                                         self.dim_k, self.dim_origin, int(accumulate),
-                                         _p(stats), 0 if stats is None else stats.shape[0],
-                                         _p(ws), wsb, ctypes.c_void_p(stream.cuda_stream)),
+                                         self.dim_k, self.dim_origin, int(accumulate), _p(st),
+                                         n_st, stride, _p(ws), wsb,
+                                         ctypes.c_void_p(stream.cuda_stream)),
               "spgemm_forward")
         self._end(stream)
         return out

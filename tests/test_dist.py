@@ -34,6 +34,10 @@ def test_partition_balances_nnz_and_remaps():
                 assert torch.equal(part.table_positions(q), pos[a:b].long())
             if phases == 1:
                 assert bool((pos[1:] > pos[:-1]).all())
+                # each rank's block ends in a spare (statistics) row no node maps to
+                spare = torch.tensor([part.stats_position(q) for q in range(w)])
+                assert not bool(torch.isin(spare, pos.long()).any())
+                assert part.padded_rows == w * (part.max_rows + 1)
             # a phase's CSR keeps exactly the edges whose column lies in that phase
             lp, li, lv = part.local_csr(ptr, idx, graphs.sage_mean_values(ptr), 0)
             tot = 0
@@ -53,7 +57,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, ret, phases=1, size=(700, 15_000)):
+def _worker(rank, world, port, ret, phases=1, size=(700, 15_000), split=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -66,33 +70,39 @@ def _worker(rank, world, port, ret, phases=1, size=(700, 15_000)):
         part = RowPartition(ptr, world, phases=phases)
         r0, r1 = part.rows(rank)
         sd, si = oracle.maxk(x[r0:r1].numpy(), k)
-        nc = part.phase_cols
 
-        def phase_graph(ph):
-            lptr, lidx, lval = part.phase_csr(shard.ptr, shard.idx, shard.val, ph)
-            # the oracle indexes CBSR rows by column id: pad the local rows to the block size
+        def part_graph(i):
+            # part i's CSR (a column phase, or the own / remote columns of the split); the
+            # oracle indexes CBSR rows by column id: pad the local rows to the table size
+            lptr, lidx, lval, nc = shard.parts[i]
             nr = max(nc, r1 - r0)
             full_ptr = np.full(nr + 1, lptr[-1].item(), np.int32)
             full_ptr[: lptr.numel()] = lptr.numpy()
-            return full_ptr, lidx.numpy(), lval.numpy(), nr
+            return full_ptr, lidx.numpy(), lval.numpy(), nr, nc
 
-        def fwd(ph, td, ti, out):
-            fp, li, lv, nr = phase_graph(ph)
+        def fwd(i, td, ti, out):
+            fp, li, lv, nr, nc = part_graph(i)
+            assert td.shape[0] == nc
             tdp = np.zeros((nr, k), np.float32)
             tip = np.zeros((nr, k), np.uint8)
             tdp[:nc], tip[:nc] = td.numpy(), ti.numpy()
             y = torch.from_numpy(oracle.spgemm_forward(fp, li, lv, tdp, tip, d)[: r1 - r0].copy())
             return y if out is None else out + y
 
-        def bwd(ph, gl, ti):
-            fp, li, lv, nr = phase_graph(ph)
+        def bwd(i, gl, ti):
+            fp, li, lv, nr, nc = part_graph(i)
             gfull = np.zeros((nr, d), np.float32)
             gfull[: r1 - r0] = gl.numpy()
             tip = np.zeros((nr, k), np.uint8)
             tip[:nc] = ti.numpy()
             return torch.from_numpy(oracle.sspmm_backward(fp, li, lv, gfull, tip)[:nc].copy())
 
-        shard = ShardedAggregation(part, rank, ptr, idx, val, d, k, fwd=fwd, bwd=bwd)
+        shard = ShardedAggregation(part, rank, ptr, idx, val, d, k, fwd=fwd, bwd=bwd,
+                                   split=split)
+        if split:   # the own-column part holds exactly the edges into this rank's rows
+            own = ((idx[int(ptr[r0]):int(ptr[r1])] >= r0) & (idx[int(ptr[r0]):int(ptr[r1])] < r1))
+            assert shard.parts[0][1].numel() == int(own.sum())
+            assert shard.parts[0][1].numel() + shard.parts[1][1].numel() == int(ptr[r1] - ptr[r0])
         y = shard.forward(torch.from_numpy(sd), torch.from_numpy(si))
         gs = shard.backward(g[r0:r1])
         ret[rank] = (r0, r1, y.numpy().copy(), gs.numpy().copy(),
@@ -101,14 +111,19 @@ def _worker(rank, world, port, ret, phases=1, size=(700, 15_000)):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,phases,size", [(2, 1, (700, 15_000)), (2, 2, (700, 15_000)),
-                                               (3, 2, (700, 15_000)),
-                                               (4, 1, (20_000, 600_000))])
-def test_sharded_aggregation_matches_single(world, phases, size):
+@pytest.mark.parametrize("world,phases,size,split", [
+    (2, 1, (700, 15_000), False), (2, 2, (700, 15_000), False), (3, 2, (700, 15_000), False),
+    (4, 1, (20_000, 600_000), False),
+    # local-columns-first split: own-column edges from the send buffers (overlapping the
+    # all-gather), remote edges accumulated on the table; own-column gradient added after the
+    # reduce-scatter
+    (2, 1, (700, 15_000), True), (3, 1, (700, 15_000), True), (4, 1, (20_000, 600_000), True)])
+def test_sharded_aggregation_matches_single(world, phases, size, split):
     from oracle import oracle
     mgr = mp.Manager()
     ret = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), ret, phases, size), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), ret, phases, size, split), nprocs=world,
+             join=True)
     (n, e), d, k = size, 32, 8
     ptr, idx = graphs.synthetic_csr(n, e, seed=3)
     val = graphs.sage_mean_values(ptr)

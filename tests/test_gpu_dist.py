@@ -77,6 +77,59 @@ def test_emulated_partition_matches_oracle(gpu, world, phases, opts, k):
     assert ok, worst
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("k", [16, 32])
+def test_emulated_shards_stats_and_split(gpu, world, split, k):
+    """ShardedAggregation as every rank builds it (statistics row in each rank's block; the
+    local-columns-first split), the all-gather emulated by filling each rank's table and
+    statistics rows, the reduce-scatter by summing the ranks' partial gradients."""
+    p, i, v = _graph()
+    n, d = p.numel() - 1, 256
+    od, oi = oracle.maxk(graphs.features(n, d, seed=15).numpy(), k)
+    g = graphs.features(n, d, seed=16)
+    ref_f, mag_f = oracle.spgemm_forward(p.numpy(), i.numpy(), v.numpy(), od, oi, d, with_mag=True)
+    ref_b, mag_b = oracle.sspmm_backward(p.numpy(), i.numpy(), v.numpy(), g.numpy(), oi,
+                                         with_mag=True)
+    ptr, idx, val = p.to(gpu), i.to(gpu), v.to(gpu)
+    sd, si, gg = torch.from_numpy(od).to(gpu), torch.from_numpy(oi).to(gpu), g.to(gpu)
+    part = RowPartition(ptr, world)
+    y = torch.empty((n, d), device=gpu)
+    grad_sum = torch.zeros((part.padded_rows, k), device=gpu)
+    for q in range(world):
+        shard = ShardedAggregation(part, q, ptr, idx, val, d, k, split=split)
+        assert shard.stats and len(shard.plans) == (2 if split else 1)
+        a, b = part.rows(q)
+        shard._stage(sd[a:b], si[a:b])
+        for r in range(world):
+            ra, rb = part.rows(r)
+            pos = part.table_positions(r, gpu)
+            shard.table_data[pos] = sd[ra:rb]
+            shard.table_index[pos] = si[ra:rb]
+            sp = part.stats_position(r)
+            shard.table_data[sp] = 0.0
+            shard.table_index[sp] = 0
+            mk.cbsr_stats(sd[ra:rb], si[ra:rb], out=shard.stats_words(shard.table_index, sp))
+        # the rank's own statistics row went out with its send buffer; its values stay zero
+        assert torch.equal(shard.send_index[part.rows_per_phase],
+                           shard.table_index[part.stats_position(q)])
+        assert not shard.send_data[part.rows_per_phase].any()
+        y[a:b] = shard.compute_forward()
+        gl = gg[a:b].contiguous()
+        if split:
+            grad_sum += shard._bwd(1, gl, shard.table_index)
+            own = shard._bwd(0, gl, shard.send_index[: shard.n_local])
+            grad_sum[part.table_positions(q, gpu)] += own[: b - a]
+        else:
+            grad_sum += shard._bwd(0, gl, shard.table_index)
+        del shard
+    gs = torch.cat([grad_sum[part.table_positions(q, gpu)] for q in range(world)])
+    ok, worst = oracle.close_enough(y.cpu().numpy(), ref_f, mag_f)
+    assert ok, worst
+    ok, worst = oracle.close_enough(gs.cpu().numpy(), ref_b, mag_b)
+    assert ok, worst
+
+
 def test_forward_accumulate_vs_oracle(gpu):
     """maxk_spgemm_forward_acc: out += A densify(sp) on top of prior values."""
     p, i, v = _graph(n=3000, e=60_000, seed=43)
@@ -104,8 +157,9 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("phases,opts", [(1, None), (2, None), (1, {"bwd_algo": 3})])
-def test_sharded_aggregation_rccl_world1(gpu, phases, opts):
+@pytest.mark.parametrize("phases,opts,split", [(1, None, False), (2, None, False),
+                                               (1, {"bwd_algo": 3}, False), (1, None, True)])
+def test_sharded_aggregation_rccl_world1(gpu, phases, opts, split):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
@@ -117,7 +171,7 @@ def test_sharded_aggregation_rccl_world1(gpu, phases, opts):
         g = graphs.features(n, d, seed=8).to(gpu)
         sd, si = mk.maxk_forward(x, k, return_index=True)
         part = RowPartition(ptr, 1, phases=phases)
-        shard = ShardedAggregation(part, 0, ptr, idx, val, d, k, plan_options=opts)
+        shard = ShardedAggregation(part, 0, ptr, idx, val, d, k, plan_options=opts, split=split)
         y = shard.forward(sd, si)
         gs = shard.backward(g)
         od, oi = sd.cpu().numpy(), si.cpu().numpy()

@@ -1,6 +1,6 @@
 """GPU, BASELINE.json full sizes (synthetic graphs with the datasets' N and E, D=256):
-parity through size-independent properties plus sampled rows/columns checked against
-the oracle. Cases follow BASELINE.json configs: Reddit SAGE-mean k=16 (the bench
+the top-k bit-exact against the oracle on every row, and the aggregation's parity through
+size-independent properties plus sampled rows/columns checked against the oracle. Cases follow BASELINE.json configs: Reddit SAGE-mean k=16 (the bench
 workload) and k=8/64, ogbn-products SAGE k=32, ogbn-proteins GCN k in {8,16,32,64}.
 
 * adjoint identity   <A densify(sp), G> == <sp_data, SSpMM(G)>   (float64 reductions)
@@ -108,3 +108,35 @@ def test_sampled_columns_vs_oracle(case):
     np.add.at(mag, c, np.abs(terms))
     ok, worst = oracle.close_enough(gs.cpu().numpy()[cols], ref[cols], mag[cols])
     assert ok, worst
+
+
+# ------------------------------------------------------------------ top-k at config size
+# north_star: "bit-exact on the top-k index output". Every BASELINE case's feature matrix
+# (N(0,1), seed 97, D=256) through maxk_forward in both modes against oracle.maxk: indices
+# and value bits equal on all N rows.
+TOPK_CASES = [("reddit", k) for k in (8, 16, 32, 64)] + [("ogbn-products", 32)] + \
+             [("ogbn-proteins", k) for k in (8, 16, 32, 64)]
+_FEATS = {}
+
+
+@pytest.mark.parametrize("mode", ["exact", "ref_compat"])
+@pytest.mark.parametrize("name,k", TOPK_CASES, ids=lambda v: str(v))
+def test_topk_bit_exact_at_config_size(gpu, name, k, mode):
+    if name not in _FEATS:
+        _FEATS.clear()                   # one feature matrix resident at a time
+        _GRAPHS.clear()
+        torch.cuda.empty_cache()
+        n, _ = graphs.DATASETS[name]
+        h = graphs.features(n, D, seed=97, device=gpu)
+        _FEATS[name] = (h, h.cpu().numpy())
+    h, hn = _FEATS[name]
+    sd, si, cnt = mk.maxk_forward(h, k, mode=mode, return_index=True, return_count=True)
+    od, oi = oracle.maxk(hn, k, mode)
+    assert np.array_equal(si.cpu().numpy(), oi)
+    assert np.array_equal(sd.cpu().numpy().view(np.uint32), od.view(np.uint32))
+    c = cnt.cpu().numpy()
+    if mode == "exact":
+        assert (c == k).all()
+    else:                                # filled slots: min(#(x > p), k); the rest (0.0f, 0)
+        filled = np.arange(k)[None, :] < c[:, None]
+        assert (od[~filled] == 0).all() and (oi[~filled] == 0).all()

@@ -219,8 +219,14 @@ def test_cbsr_stats_and_forward_ex_split(gpu):
     od[10, :] = 0.0                          # an empty row
     st = mk.cbsr_stats(dev(od, gpu), dev(oi, gpu)).cpu().numpy().view(np.uint32)[0]
     mx, mn = _stats_numpy(od, oi)
-    assert st[0] == np.float32(mx).view(np.uint32)
+    # the repeated row's bound is its f32 sum of |x| (+2^-10), summed in the kernel's order
+    got = float(np.uint32(st[0]).view(np.float32))
+    assert mx * (1 - 2.0 ** -20) <= got <= mx * (1 + 2.0 ** -20)
     assert st[1] == 0x7FFFFFFF - np.float32(mn).view(np.uint32)
+    # without the repeat the bound is exactly the max |x|
+    oi2 = oracle.maxk(graphs.features(n, d, seed=77).numpy(), k)[1]
+    st2 = mk.cbsr_stats(dev(od, gpu), dev(oi2, gpu)).cpu().numpy().view(np.uint32)[0]
+    assert st2[0] == np.abs(od).max().view(np.uint32)
     # the stats of two halves of the table, as the multi-GPU path gathers them per rank
     sd, si = dev(od, gpu), dev(oi, gpu)
     halves = torch.cat([mk.cbsr_stats(sd[:1500], si[:1500]), mk.cbsr_stats(sd[1500:], si[1500:])])
@@ -266,3 +272,24 @@ def test_auto_row_order_follows_dense_runs(gpu):
         p, ix, v = graph(name)
         plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), p.size - 1, ix.size, 256, 16)
         assert plan.info()["bwd_row_order"] == want, name
+
+
+@pytest.mark.parametrize("k", [8, 16, 12, 20, 10])
+def test_cbsr_stats_repeat_detection(gpu, k):
+    """A repeated selector is found whatever lies between the two entries (zeros, other lanes'
+    entries); zero padding after the filled slots (ref_compat rows) is not a repeat."""
+    base = np.arange(1, k + 1, dtype=np.int64) * 3
+    cases = []
+    s = base.copy(); s[2] = s[0]; cases.append((s, np.ones(k), True))            # same lane
+    s = base.copy(); s[k - 1] = s[0]; cases.append((s, np.ones(k), True))        # far lanes
+    s = base.copy(); s[1] = 1; s[2] = s[0]; x = np.ones(k); x[1] = 0.0           # zero between
+    cases.append((s, x, True))
+    s = base.copy(); s[k // 2:] = 0; x = np.ones(k); x[k // 2:] = 0.0            # padding
+    cases.append((s, x, False))
+    cases.append((base.copy(), np.ones(k), False))                              # ascending
+    for s, x, rep in cases:
+        xs = (x * np.linspace(1.0, 2.0, k)).astype(np.float32)[None, :]
+        st = mk.cbsr_stats(dev(xs, gpu), dev(s.astype(np.uint8)[None, :], gpu))
+        got = float(np.uint32(st.cpu().numpy().view(np.uint32)[0, 0]).view(np.float32))
+        want = xs.sum() * (1 + 2.0 ** -10) if rep else xs.max()
+        assert abs(got - want) <= 1e-6 * want, (k, s, x, got, want)

@@ -33,4 +33,10 @@ for _ in range(3):
 for _ in range(3):
     plan.backward(g, sp_index, grad)
 torch.cuda.synchronize()
+# the kernel binary these counters belong to (tools/pmc_traffic.py stores it with the entry;
+# bench.py drops a traffic figure whose binary differs from the one it loaded)
+out_dir = os.environ.get("PMC_OUT")
+if out_dir:
+    with open(os.path.join(out_dir, "lib_sha256.txt"), "w") as f:
+        f.write(mk._lib.lib_sha256() + "\n")
 print("done", plan.info())

@@ -4,6 +4,7 @@
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out/pmc${PMC_TAG}"
 mkdir -p "$OUT"
+export PMC_OUT="$OUT"
 cd /tmp && export TMPDIR=/tmp
 i=0
 while read -r counters; do

@@ -52,6 +52,9 @@ def collect(root):
 def entry_for(root):
     vals, durs = collect(root)
     entry = {}
+    sha = os.path.join(root, "lib_sha256.txt")
+    # the libmaxk_hip.so the counters were collected on (tools/pmc_driver.py)
+    entry["lib_sha256"] = open(sha).read().strip() if os.path.exists(sha) else None
     fam_bytes = {}
     fam_secs = {}
     for fam, cs in vals.items():

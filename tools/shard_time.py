@@ -1,8 +1,13 @@
 """Per-rank device time of the row-partitioned path on ONE GPU (tooling): for W in 1,2,4,8
-build each rank's rectangular plan exactly as maxk_kernels.dist does and time its SpGEMM
-forward + SSpMM backward (no collectives), to see how the compute part strong-scales.
+build ranks' ShardedAggregation exactly as maxk_kernels.dist does, fill their gathered
+tables (and statistics rows) as the all-gather would, and time the forward and backward
+kernels alone (compute_forward / compute_backward: no collectives), to see how the compute
+part strong-scales and what the variants cost:
 
-  python tools/shard_time.py [--k 16]
+  stats   : the forward reads the W gathered statistics pairs (default) / scans the table
+  split   : the local-columns-first split (two plans per rank) / one plan
+
+  python tools/shard_time.py [--k 16] [--worlds 1,2,4,8] [--variants '[...]']
 """
 import argparse
 import json
@@ -16,18 +21,21 @@ import torch  # noqa: E402
 
 import maxk_kernels as mk  # noqa: E402
 from maxk_kernels import graphs  # noqa: E402
-from maxk_kernels.dist import RowPartition  # noqa: E402
+from maxk_kernels.dist import RowPartition, ShardedAggregation  # noqa: E402
 
 
-def timeit(fn, reps=10):
+def timeit(fn, reps=20, rounds=3):
     fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps
+    ts = []
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e) / reps)
+    return sorted(ts)[len(ts) // 2]
 
 
 def main():
@@ -35,8 +43,10 @@ def main():
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--dataset", default="reddit")
     ap.add_argument("--worlds", default="1,2,4,8")
-    ap.add_argument("--phases", default="1", help="column phases to compare, e.g. 1,2")
-    ap.add_argument("--opts", default="[{}]", help="JSON list of plan option dicts to compare")
+    ap.add_argument("--variants", default='[{"split": false, "stats": true}, '
+                                          '{"split": false, "stats": false}, '
+                                          '{"split": true, "stats": true}]')
+    ap.add_argument("--opts", default="{}", help="plan options (JSON dict)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS[args.dataset]
@@ -46,49 +56,39 @@ def main():
     h = graphs.features(n, d, seed=97, device=dev)
     g = graphs.features(n, d, seed=98, device=dev)
     sd, si = mk.maxk_forward(h, k, return_index=True)
-    for world, phases, opts in [(int(w), int(ph), o) for w in args.worlds.split(",")
-                                for ph in args.phases.split(",") for o in json.loads(args.opts)]:
-        part = RowPartition(ptr, world, phases=phases)
-        td = torch.zeros((part.padded_rows, k), device=dev)
-        tix = torch.zeros((part.padded_rows, k), dtype=torch.uint8, device=dev)
-        for q in range(world):
-            a, b = part.rows(q)
-            pos = part.table_positions(q, dev)
-            td[pos] = sd[a:b]
-            tix[pos] = si[a:b]
-        nc = part.phase_cols
-        worst = 0.0
-        for q in (0, world - 1):
-            a, b = part.rows(q)
-            lp, li, lv = part.local_csr(ptr, idx, val, q)
-            plans = []
-            for ph in range(phases):
-                pp, pi, pv = part.phase_csr(lp, li, lv, ph)
-                plans.append(mk.GraphPlan(pp, pi, pv, b - a, pi.numel(), d, k, num_cols=nc,
-                                          options=opts))
-            gl = g[a:b].contiguous()
-            out = torch.empty((b - a, d), device=dev)
-            gr = torch.empty((part.padded_rows, k), device=dev)
-
-            def fwd():
-                for ph, pl in enumerate(plans):
-                    pl.forward(td[ph * nc:(ph + 1) * nc], tix[ph * nc:(ph + 1) * nc], out,
-                               accumulate=ph > 0)
-
-            def bwd():
-                for ph, pl in enumerate(plans):
-                    pl.backward(gl, tix[ph * nc:(ph + 1) * nc], gr[ph * nc:(ph + 1) * nc])
-
-            tf = timeit(fwd)
-            tb = timeit(bwd)
-            worst = max(worst, tf + tb)
-            print(json.dumps({"world": world, "phases": phases, "opts": opts, "rank": q,
-                              "edges": li.numel(), "fwd_ms": tf, "bwd_ms": tb,
-                              "info": plans[0].info()}), flush=True)
-            del plans
-        print(json.dumps({"world": world, "phases": phases, "opts": opts,
-                          "compute_ms_max": worst,
-                          "edges_per_s_compute_only": 2 * e / (worst * 1e-3)}), flush=True)
+    del h
+    opts = json.loads(args.opts)
+    for world in [int(w) for w in args.worlds.split(",")]:
+        part = RowPartition(ptr, world)
+        for var in json.loads(args.variants):
+            worst = 0.0
+            for q in sorted({0, world - 1}):
+                shard = ShardedAggregation(part, q, ptr, idx, val, d, k, plan_options=opts,
+                                           split=var["split"])
+                a, b = part.rows(q)
+                shard._stage(sd[a:b], si[a:b])          # send buffers + this rank's stats row
+                shard.table_data.zero_()                # spare rows: zeros, as gathered
+                shard.table_index.zero_()
+                for r in range(world):                  # the all-gather, emulated
+                    ra, rb = part.rows(r)
+                    pos = part.table_positions(r, dev)
+                    shard.table_data[pos] = sd[ra:rb]
+                    shard.table_index[pos] = si[ra:rb]
+                    if shard.stats:
+                        mk.cbsr_stats(sd[ra:rb], si[ra:rb],
+                                      out=shard.stats_words(shard.table_index,
+                                                            part.stats_position(r)))
+                shard.stats = shard.stats and var["stats"]
+                gl = g[a:b].contiguous()
+                tf = timeit(shard.compute_forward)
+                tb = timeit(lambda: shard.compute_backward(gl))
+                worst = max(worst, tf + tb)
+                print(json.dumps({"world": world, **var, "opts": opts, "rank": q,
+                                  "edges": int(shard.ptr[-1]), "fwd_ms": tf, "bwd_ms": tb,
+                                  "plans": [p.info() for p in shard.plans]}), flush=True)
+                del shard
+            print(json.dumps({"world": world, **var, "opts": opts, "compute_ms_max": worst,
+                              "edges_per_s_compute_only": 2 * e / (worst * 1e-3)}), flush=True)
 
 
 if __name__ == "__main__":
