@@ -255,6 +255,6 @@ struct maxk_plan {
   int32_t external_ws = 0;
   int64_t fwd_ws_bytes = 0;
   int64_t bwd_ws_bytes = 0;
-  int32_t bwd_chunk_mode = 3;    // chunk bounds in use: 1 shared rows, 2 equal edges, 3 cost
+  int32_t bwd_chunk_mode = 2;    // chunk bounds in use: 1 shared rows, 2 equal edges, 3 cost
   int32_t bwd_row_order = 1;     // rows in the block streams: 1 ascending, 2 scattered
 };

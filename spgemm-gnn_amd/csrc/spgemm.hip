@@ -1466,8 +1466,10 @@ static int launch_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int6
   if (nrows <= 0) return MAXK_OK;
   if (k % 4 == 0) {
     const int64_t rows_per_block = (256 / kWave) * (kWave / (k / 4));
+    // one work-group per CU: each adds one atomic per word, and same-address atomics from
+    // every work-group serialise at the L2
     const int grid = (int)std::max<int64_t>(
-        1, std::min<int64_t>((nrows + rows_per_block - 1) / rows_per_block, 4 * cus));
+        1, std::min<int64_t>((nrows + rows_per_block - 1) / rows_per_block, cus));
     hipLaunchKernelGGL(cbsr_stats4_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nrows,
                        k, st0, st1);
   } else {

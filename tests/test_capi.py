@@ -202,3 +202,36 @@ def test_header_is_plain_c(tmp_path):
     r = subprocess.run([cc, "-std=c99", "-Wall", "-Werror", "-pedantic", "-fsyntax-only",
                         "-I", os.path.dirname(HEADER), str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_plan_create_sized_option_sizes():
+    """maxk_plan_create_sized reads opts_bytes of the caller's options: a smaller (older)
+    struct leaves the rest at 0, a larger (newer) one must have its extra fields at 0, and the
+    size must be whole int32 fields. All rejected on the host, before any device call."""
+    opts = _lib.PlanOptions()
+    size = ctypes.sizeof(opts)
+    h = ctypes.c_void_p(0)
+    lib = _lib.lib
+    args = (None, None, None, 10, 10, 100, 256, 16)
+    assert lib.maxk_plan_create_sized(*args, ctypes.byref(opts), 6, None, None,
+                                      ctypes.byref(h)) == -1
+    assert "multiple of 4" in lib.maxk_last_error().decode()
+    bigger = (ctypes.c_uint8 * (size + 8))()
+    bigger[size + 4] = 1                              # a field this library does not know
+    assert lib.maxk_plan_create_sized(*args, ctypes.cast(bigger, ctypes.c_void_p), size + 8,
+                                      None, None, ctypes.byref(h)) == -1
+    assert "newer" in lib.maxk_last_error().decode()
+    bigger[size + 4] = 0                              # zero extra fields are accepted ...
+    assert lib.maxk_plan_create_sized(*args, ctypes.cast(bigger, ctypes.c_void_p), size + 8,
+                                      None, None, ctypes.byref(h)) == -1
+    assert "null pointer" in lib.maxk_last_error().decode()   # ... then ptr = NULL is refused
+    # the version-1 layout is 120 bytes (round-1 options, up to fwd_rot_rate)
+    assert _lib.PlanOptions.bwd_flush.offset == 31 * 4 and _lib.PlanOptions.external_workspace.offset == 120
+    # an ABI-2 option (col_order = 4) needs the permutation argument
+    opts.col_order = 4
+    assert lib.maxk_plan_create_sized(*args, ctypes.byref(opts), size, None, None,
+                                      ctypes.byref(h)) == -1
+    assert "col_order" in lib.maxk_last_error().decode()
+    assert not h.value
+    info = _lib.PlanInfo()
+    assert lib.maxk_plan_get_info_sized(None, ctypes.byref(info), ctypes.sizeof(info)) == -1
