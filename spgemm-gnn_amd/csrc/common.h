@@ -60,6 +60,11 @@ constexpr double kBwdTwoPassWorkspaceCap = 16.0 * (1ull << 30);
 // quarter-edges ran 2.13, 2.03, 1.95, 2.07, 2.30 ms (equal edges 2.19); uniform graphs are
 // within +-0.3 % of equal edges at every value
 constexpr int kBwdRowCost4 = 8;
+// work-groups per CU of the fused CBSR pack + statistics pass (each adds one atomic per
+// statistics word, and same-address atomics serialise at the L2). Reddit, pack+stats at
+// k = 16 / stats at k = 32, 64: 1 -> 24.5 / 54.5 us, 4 -> 20.8 / 26.6 us, 8 -> 31.5 / 33.7 us
+// (the separate pack + stats passes took 21 + 17 us at k = 16)
+constexpr int kStatsBlocksPerCu = 4;
 constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (plan: 2 at k >= 32 with
                                      // few edges per block row)
 // Records past the end of the backward edge list that a wave may read (and ignore).

@@ -139,10 +139,16 @@ __device__ __forceinline__ double fwd_fix_scale(int2 fix, const uint32_t* xs, in
 // whether a lane's first nonzero selector is <= the last nonzero selector of any earlier lane
 // (or its own nonzero selectors do not ascend): the same bound as the thread-per-row kernel
 // below, with the row sum added in another order (its 2^-10 headroom covers that).
+//
+// PACK: the same pass also writes the forward's packed CBSR records (pack_cbsr_kernel's
+// layout: k values, then the k selector bytes, rec_bytes per row), so the per-call pack and
+// the statistics cost one read of the tables. STATS = false: the pack alone.
+template <bool PACK, bool STATS>
 __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restrict__ x,
                                                           const uint8_t* __restrict__ sel,
                                                           int64_t nrows, int k, uint32_t* st0,
-                                                          uint32_t* st1) {
+                                                          uint32_t* st1, uint8_t* __restrict__ rec,
+                                                          int rec_bytes) {
   __shared__ uint32_t smx[256 / kWave], smn[256 / kWave];
   const int L = k >> 2;
   const int RW = kWave / L;  // rows per wave
@@ -160,7 +166,13 @@ __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restric
     if (live) {
       v = *reinterpret_cast<const float4*>(x + r * k + 4 * q);
       s = *reinterpret_cast<const uint32_t*>(sel + r * k + 4 * q);
+      if constexpr (PACK) {
+        uint8_t* rp = rec + r * rec_bytes;
+        *reinterpret_cast<float4*>(rp + 16 * q) = v;
+        *reinterpret_cast<uint32_t*>(rp + 4 * k + 4 * q) = s;
+      }
     }
+    if constexpr (!STATS) continue;
     const uint32_t b[4] = {__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu,
                            __float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu};
     uint32_t lmax = 0u, lmin = 0x7fffffffu;
@@ -210,6 +222,7 @@ __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restric
       }
     }
   }
+  if constexpr (!STATS) return;
   for (int o = kWave / 2; o > 0; o >>= 1) {
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
     mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
@@ -295,21 +308,7 @@ __global__ __launch_bounds__(256) void cbsr_stats_kernel(const float* __restrict
 // node, {k values, k selectors, pad} of rec_bytes (128 B at k = 16): one line per edge.
 // On gfx950 the gather is bound by L1/TA request count, not by bytes or by where the line
 // is served from (tools/ubench_gather.hip: 2.70 ms -> 1.84 ms for Reddit at k = 16).
-__global__ void pack_cbsr_kernel(const float* __restrict__ sp_data,
-                                 const uint8_t* __restrict__ sp_index,
-                                 uint8_t* __restrict__ rec, int ncols, int k, int rec_bytes) {
-  const int words = k + k / 4;  // k value words + k/4 selector words (k % 4 == 0)
-  const int64_t total = (int64_t)ncols * words;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t c = t / words;
-    const int w = (int)(t - c * words);
-    uint32_t v;
-    if (w < k) v = __float_as_uint(sp_data[c * k + w]);
-    else v = reinterpret_cast<const uint32_t*>(sp_index + c * k)[w - k];
-    reinterpret_cast<uint32_t*>(rec + c * rec_bytes)[w] = v;
-  }
-}
+// cbsr_stats4_kernel<PACK = true> writes them (k % 4 == 0), fused with the statistics.
 
 // Lane-chunk CBSR records (plan->fwd_chunk3): chunk j of column c is 16 B, {x[3j],
 // x[3j+1], x[3j+2], selectors 3j..3j+2 in bytes 0..2 of the 4th word}, so ONE dwordx4 gather
@@ -1461,17 +1460,28 @@ using namespace maxk;
 
 // Fixed-point statistics of a CBSR table into two zeroed words: the lane-parallel kernel
 // for k % 4 == 0 (~10 us for Reddit at k = 16), one thread per row otherwise.
+// rec != nullptr (k % 4 == 0 only): also pack the forward's CBSR records (st0 == nullptr: the
+// pack alone)
 static int launch_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int64_t nrows, int k,
-                             uint32_t* st0, uint32_t* st1, int cus, hipStream_t s) {
+                             uint32_t* st0, uint32_t* st1, int cus, hipStream_t s,
+                             uint8_t* rec = nullptr, int rec_bytes = 0) {
   if (nrows <= 0) return MAXK_OK;
   if (k % 4 == 0) {
     const int64_t rows_per_block = (256 / kWave) * (kWave / (k / 4));
-    // one work-group per CU: each adds one atomic per word, and same-address atomics from
-    // every work-group serialise at the L2
+    // statistics: one work-group per CU, each adds one atomic per word, and same-address
+    // atomics from every work-group serialise at the L2; the pack alone: more in flight
+    const int cap = st0 ? cus * kStatsBlocksPerCu : 8 * cus;
     const int grid = (int)std::max<int64_t>(
-        1, std::min<int64_t>((nrows + rows_per_block - 1) / rows_per_block, cus));
-    hipLaunchKernelGGL(cbsr_stats4_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nrows,
-                       k, st0, st1);
+        1, std::min<int64_t>((nrows + rows_per_block - 1) / rows_per_block, cap));
+    if (rec && st0)
+      hipLaunchKernelGGL((cbsr_stats4_kernel<true, true>), dim3(grid), dim3(256), 0, s, sp_data,
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes);
+    else if (rec)
+      hipLaunchKernelGGL((cbsr_stats4_kernel<true, false>), dim3(grid), dim3(256), 0, s, sp_data,
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes);
+    else
+      hipLaunchKernelGGL((cbsr_stats4_kernel<false, true>), dim3(grid), dim3(256), 0, s, sp_data,
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes);
   } else {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nrows + 255) / 256, 2 * cus));
     hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nrows,
@@ -1537,25 +1547,12 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   const uint8_t* seltab = two ? sp_index : nullptr;
   const uint8_t* recp = two ? reinterpret_cast<const uint8_t*>(sp_data) : rec_ws;
   const int rec_bytes_eff = two ? 4 * k : rec_bytes;
-  if (two) {
-    // nothing to pack
-  } else if (plan->fwd_chunk3 && plan->num_cols > 0) {
-    const int64_t items = (int64_t)plan->num_cols * ((k + 2) / 3);
-    const int grid = (int)std::min<int64_t>((items + 255) / 256, 65536);
-    hipLaunchKernelGGL(pack_cbsr3_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
-                       rec_ws, plan->num_cols, k, rec_bytes);
-    MAXK_LAUNCH_CHECK("pack_cbsr3 launch");
-  } else if (k % 4 == 0 && plan->num_cols > 0) {
-    const int64_t words = (int64_t)plan->num_cols * (k + k / 4);
-    const int grid = (int)std::min<int64_t>((words + 255) / 256, 65536);
-    hipLaunchKernelGGL(pack_cbsr_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
-                       rec_ws, plan->num_cols, k, rec_bytes);
-    MAXK_LAUNCH_CHECK("pack_cbsr launch");
-  }
   // fixed-point forward: the call's slot bound / min |x| for fwd_fix_scale (one pass over the
-  // CBSR table), or the caller's per-rank pairs (maxk_spgemm_forward_ex)
+  // CBSR table, fused with the record pack when there is one), or the caller's per-rank pairs
+  // (maxk_spgemm_forward_ex)
   const int2* fix_tab = nullptr;
   const uint32_t* xstat = nullptr;
+  uint32_t* st = nullptr;
   int xs_n = 1, xs_stride = 0, xs_off2 = 32;
   if (plan->fwd_fix && plan->num_cols > 0) {
     fix_tab = plan->fwd_fix;
@@ -1565,13 +1562,24 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       xs_stride = (int)stats_stride;
       xs_off2 = 1;
     } else {
-      uint32_t* st = reinterpret_cast<uint32_t*>(ws_base + plan->fwd_xstat_off);
+      st = reinterpret_cast<uint32_t*>(ws_base + plan->fwd_xstat_off);
       MAXK_HIP_TRY(hipMemsetAsync(st, 0, 256, s));
-      const int rc = launch_cbsr_stats(sp_data, sp_index, plan->num_cols, k, st, st + 32,
-                                       plan->cus, s);
-      if (rc) return rc;
       xstat = st;
     }
+  }
+  const bool pack4 = !two && !plan->fwd_chunk3 && k % 4 == 0 && plan->num_cols > 0;
+  if (plan->fwd_chunk3 && plan->num_cols > 0) {
+    const int64_t items = (int64_t)plan->num_cols * ((k + 2) / 3);
+    const int grid = (int)std::min<int64_t>((items + 255) / 256, 65536);
+    hipLaunchKernelGGL(pack_cbsr3_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
+                       rec_ws, plan->num_cols, k, rec_bytes);
+    MAXK_LAUNCH_CHECK("pack_cbsr3 launch");
+  }
+  if (pack4 || st) {
+    const int rc = launch_cbsr_stats(sp_data, sp_index, plan->num_cols, k, st,
+                                     st ? st + 32 : nullptr, plan->cus, s,
+                                     pack4 ? rec_ws : nullptr, rec_bytes);
+    if (rc) return rc;
   }
   const int rot = plan->fwd_rot_ticks;
   // persistent grid: as many work-groups as fit on the device at once (capped by tasks)
