@@ -163,8 +163,8 @@ def main():
                          "one phase overlapping the other's compute; 1 = one-shot, the default: "
                          "2 phases cost +14 %% per-rank compute at W=8, tools/shard_time.py)")
     ap.add_argument("--split", action="store_true",
-                    help="N > 1: local-columns-first split (own-column edges computed while the "
-                         "all-gather / reduce-scatter are in flight; maxk_kernels.dist)")
+                    help="N > 1: local-columns-first split of the forward (own-column edges "
+                         "computed while the all-gather is in flight; maxk_kernels.dist)")
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--cpu-sample", type=float, default=1.0,
                     help="fraction of E timed per direction for the CPU baseline")
@@ -461,9 +461,9 @@ def main():
         result["k_sweep"] = dict(sorted(sweep.items(), key=lambda kv: int(kv[0])))
 
     if rank == 0 and world == 1 and not args.no_comparator:
-        # rocSPARSE CSR SpMM on the dense MaxK output: the reference's cuSPARSE comparator
-        # (spmm_cusparse SO@0x243a0) called directly (best of its CSR algorithms), and the
-        # same product through torch.sparse
+        # rocSPARSE SpMM on the dense MaxK output: the reference's cuSPARSE comparators
+        # (spmm_cusparse SO@0x243a0, spmm_cusparse_coo SO@0x24700) called directly (best of
+        # the CSR and COO algorithms), and the same product through torch.sparse
         from maxk_kernels import baselines
         comp = {}
         x = torch.zeros((n, d), dtype=torch.float32, device=dev)
@@ -474,6 +474,14 @@ def main():
                 comp[f"rocsparse_spmm_{alg}_ms"] = ms
             except Exception as exc:  # pragma: no cover - library/alg availability
                 comp[f"rocsparse_spmm_{alg}_error"] = repr(exc)[:160]
+        rows = baselines.coo_rows(ptr)   # spmm_cusparse_coo (SO@0x24700): the COO form
+        for alg in ("coo_segmented", "coo_atomic"):
+            try:
+                _, ms = baselines.spmm_rocsparse_coo(rows, idx, val, x, times=5, alg=alg)
+                comp[f"rocsparse_spmm_{alg}_ms"] = ms
+            except Exception as exc:  # pragma: no cover - library/alg availability
+                comp[f"rocsparse_spmm_{alg}_error"] = repr(exc)[:160]
+        del rows
         best = [v for kk, v in comp.items() if kk.endswith("_ms")]
         if best:
             comp["rocsparse_spmm_best_ms"] = min(best)

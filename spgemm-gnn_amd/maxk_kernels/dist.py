@@ -21,11 +21,14 @@ selector bytes of that row (``maxk_cbsr_stats``: two words; the value row stays 
 row adds nothing anywhere), the gathered index table carries one pair per rank and the
 forward reads those W pairs (``maxk_spgemm_forward_ex``) instead of scanning the whole table.
 
-Local-columns-first split (``split=True``, one phase): the rank's edges are cut into those
-whose column it owns and the rest, with a plan each. The forward runs the local plan on the
-send buffers while the all-gather is in flight, then the remote plan accumulates on the
-gathered table. The backward runs the remote plan, starts the reduce-scatter, runs the local
-plan while it is in flight, and adds the local gradient to the scattered one.
+Local-columns-first split (``split=True``, one phase, forward only): the rank's edges are
+cut into those whose column it owns and the rest, with a plan each. The forward runs the
+local plan on the send buffers while the all-gather is in flight, then the remote plan
+accumulates on the gathered table. The backward runs one plan over all the rank's edges and
+then the reduce-scatter: splitting it too (remote plan, reduce-scatter in flight while the
+local plan runs) cost more than the exchange it hides (Reddit k=16, one rank of W=2 / 8:
+0.88 -> 1.34 ms / 0.23 -> 0.32 ms, ``tools/shard_time.py``), since each part's column
+blocks see half as many edges per grad_out row.
 
 Column phases (``phases`` P > 1): every rank's rows are cut into P parts and the table is
 laid out phase-major (phase p holds part p of every rank), so each phase is one all-gather
@@ -172,9 +175,10 @@ class ShardedAggregation:
         if self.split:
             lo = rank * part.phase_rows
             own = (self.idx >= lo) & (self.idx < lo + self.n_local)
+            # own columns, remote columns (forward), all edges (backward)
             self.parts = [select_csr(self.ptr, self.idx, self.val, own, lo) + (max(1, self.n_local),),
-                          select_csr(self.ptr, self.idx, self.val, ~own) + (part.padded_rows,)]
-            self.grad_own = torch.empty((max(1, self.n_local), k), dtype=torch.float32, device=dev)
+                          select_csr(self.ptr, self.idx, self.val, ~own) + (part.padded_rows,),
+                          (self.ptr, self.idx, self.val, part.padded_rows)]
         else:
             self.parts = [part.phase_csr(self.ptr, self.idx, self.val, p) + (part.phase_cols,)
                           for p in range(P)]
@@ -209,7 +213,7 @@ class ShardedAggregation:
 
     def _grad_dst(self, i):
         if self.split:
-            return self.grad_own if i == 0 else self.grad_table
+            return self.grad_table
         return self._slice(self.grad_table, i)
 
     @property
@@ -294,15 +298,10 @@ class ShardedAggregation:
 
     def backward(self, grad_out_local: torch.Tensor) -> torch.Tensor:
         g = grad_out_local.contiguous()
-        if self.split:
-            # remote columns first; the own columns' gradient stays here and is computed
-            # while the reduce-scatter is in flight (its slot in the scatter holds zeros)
-            gp = self._bwd(1, g, self.table_index)
-            wk = dist.reduce_scatter_tensor(self.grad_local, gp, op=dist.ReduceOp.SUM,
-                                            group=self.group, async_op=True)
-            gl = self._bwd(0, g, self.send_index[: self.n_local])
-            wk.wait()
-            self.grad_local[: self.n_local].add_(gl[: self.n_local])
+        if self.split:  # the all-edges plan, then the one-shot reduce-scatter
+            gp = self._bwd(2, g, self.table_index)
+            dist.reduce_scatter_tensor(self.grad_local, gp, op=dist.ReduceOp.SUM,
+                                       group=self.group)
             return self.grad_local[: self.n_local]
         works = []
         for p in range(self.part.phases):
@@ -318,8 +317,7 @@ class ShardedAggregation:
         """The backward's kernels alone (no exchange): per-rank timing."""
         g = grad_out_local.contiguous()
         if self.split:
-            self._bwd(1, g, self.table_index)
-            self._bwd(0, g, self.send_index[: self.n_local])
+            self._bwd(2, g, self.table_index)
             return
         for p in range(self.part.phases):
             self._bwd(p, g, self._slice(self.table_index, p))

@@ -149,7 +149,8 @@ def test_baseline_library_exports_its_header():
     header = os.path.join(ROOT, "include", "maxk_baseline.h")
     text = re.sub(r"/\*.*?\*/", "", open(header).read(), flags=re.S)
     names = sorted(set(re.findall(r"\b(maxk_\w+)\s*\(", text)))
-    assert names == ["maxk_baseline_last_error", "maxk_spmm_rocsparse"]
+    assert names == ["maxk_baseline_last_error", "maxk_spmm_rocsparse",
+                     "maxk_spmm_rocsparse_coo"]
     lib = ctypes.CDLL(os.path.join(os.path.dirname(_lib.LIB_PATH), "libmaxk_baseline.so"))
     for n in names:
         assert hasattr(lib, n), n
@@ -158,6 +159,9 @@ def test_baseline_library_exports_its_header():
     ms = ctypes.c_float()
     assert bl.maxk_spmm_rocsparse(None, None, None, None, None, -1, 0, 8, 0, 0,
                                   ctypes.byref(ms), None) == -1
+    assert bl.maxk_spmm_rocsparse_coo(None, None, None, None, None, 4, -1, 8, 0, 0,
+                                      ctypes.byref(ms), None) == -1
+    assert b"maxk_spmm_rocsparse_coo" in bl.maxk_baseline_last_error()
 
 
 def _struct_fields(name):

@@ -115,8 +115,7 @@ def _worker(rank, world, port, ret, phases=1, size=(700, 15_000), split=False):
     (2, 1, (700, 15_000), False), (2, 2, (700, 15_000), False), (3, 2, (700, 15_000), False),
     (4, 1, (20_000, 600_000), False),
     # local-columns-first split: own-column edges from the send buffers (overlapping the
-    # all-gather), remote edges accumulated on the table; own-column gradient added after the
-    # reduce-scatter
+    # all-gather), remote edges accumulated on the table; the backward over all edges
     (2, 1, (700, 15_000), True), (3, 1, (700, 15_000), True), (4, 1, (20_000, 600_000), True)])
 def test_sharded_aggregation_matches_single(world, phases, size, split):
     from oracle import oracle

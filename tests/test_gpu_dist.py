@@ -98,7 +98,7 @@ def test_emulated_shards_stats_and_split(gpu, world, split, k):
     grad_sum = torch.zeros((part.padded_rows, k), device=gpu)
     for q in range(world):
         shard = ShardedAggregation(part, q, ptr, idx, val, d, k, split=split)
-        assert shard.stats and len(shard.plans) == (2 if split else 1)
+        assert shard.stats and len(shard.plans) == (3 if split else 1)
         a, b = part.rows(q)
         shard._stage(sd[a:b], si[a:b])
         for r in range(world):
@@ -116,12 +116,7 @@ def test_emulated_shards_stats_and_split(gpu, world, split, k):
         assert not shard.send_data[part.rows_per_phase].any()
         y[a:b] = shard.compute_forward()
         gl = gg[a:b].contiguous()
-        if split:
-            grad_sum += shard._bwd(1, gl, shard.table_index)
-            own = shard._bwd(0, gl, shard.send_index[: shard.n_local])
-            grad_sum[part.table_positions(q, gpu)] += own[: b - a]
-        else:
-            grad_sum += shard._bwd(0, gl, shard.table_index)
+        grad_sum += shard._bwd(2 if split else 0, gl, shard.table_index)
         del shard
     gs = torch.cat([grad_sum[part.table_positions(q, gpu)] for q in range(world)])
     ok, worst = oracle.close_enough(y.cpu().numpy(), ref_f, mag_f)

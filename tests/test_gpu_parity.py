@@ -645,6 +645,23 @@ def test_rocsparse_comparator_vs_oracle(gpu):
     assert_close(y, ref, mag, rtol=2e-6 * 64)
 
 
+
+@pytest.mark.parametrize("alg", ["default", "coo_segmented", "coo_atomic", "coo_segmented_atomic"])
+def test_rocsparse_coo_comparator_vs_oracle(gpu, alg):
+    from maxk_kernels import baselines
+    p, ix, v = GRAPHS["synthetic"]()
+    n = p.size - 1
+    x = graphs.features(n, 64, seed=4)
+    ref = oracle.dense_spmm(p, ix, v, x.numpy())
+    mag = oracle.dense_spmm(p, ix, np.abs(v), np.abs(x.numpy()))
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    rows = baselines.coo_rows(ptr)
+    assert rows.numel() == idx.numel()
+    y, ms = baselines.spmm_rocsparse_coo(rows, idx, val, x.to(gpu), times=2, alg=alg)
+    assert ms > 0
+    assert_close(y, ref, mag, rtol=2e-6 * 64)
+
+
 # ------------------------------------------------------------------------ streams / scratch
 def test_two_streams_share_one_plan(gpu):
     """One cached plan used from two streams at once: each call takes its scratch (packed
