@@ -1,6 +1,7 @@
 """Small fixed workload for rocprofv3 --pmc passes (tooling): one dataset-shaped synthetic
-graph (PMC_DATASET, default reddit), D=256, k=PMC_K, SAGE-mean or GCN values (PMC_KIND),
-1 + 3 SpGEMM forwards and 1 + 3 SSpMM backwards with the default (or PMC_OPTS) plan."""
+graph (PMC_DATASET, default reddit; PMC_GRAPH uniform (default), community or shuffled as in
+tools/locality_graphs.py), D=256, k=PMC_K, SAGE-mean or GCN values (PMC_KIND), 1 + 3 SpGEMM
+forwards and 1 + 3 SSpMM backwards with the default (or PMC_OPTS) plan."""
 import json
 import os
 import sys
@@ -17,7 +18,11 @@ ds = os.environ.get("PMC_DATASET", "reddit")
 kind = os.environ.get("PMC_KIND", "sage")
 dev = torch.device("cuda:0")
 n, e = graphs.DATASETS[ds]
-ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+shape = os.environ.get("PMC_GRAPH", "uniform")
+if shape == "uniform":
+    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+else:
+    ptr, idx = graphs.community_csr(n, e, shuffle=shape == "shuffled", device=dev)
 val = graphs.sage_mean_values(ptr) if kind == "sage" else graphs.gcn_values(ptr, idx)
 e = idx.numel()
 h = graphs.features(n, 256, seed=97, device=dev)

@@ -2,13 +2,15 @@
 
   python tools/pmc_traffic.py gpurun_out/pmc [--key reddit:k16:d256:n1]
   python tools/pmc_traffic.py --all gpurun_out      (every gpurun_out/pmc_<ds>_<kind>_k<k>)
+  python tools/pmc_traffic.py --locality gpurun_out (gpurun_out/pmc_loc_* -> profiles/r03/pmc_locality.json)
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch. MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE reports half the bytes of a 16-B-per-lane streaming read on gfx950, so it is doubled;
 WRITE_SIZE is exact for streaming stores and float atomics. Both count L2 memory-side requests,
 so Infinity-Cache hits are included: the figure is L2-miss traffic (upper bound on HBM bytes).
 
-Per kernel family (pack_cbsr, spgemm_fwd, pack_sel, sspmm_bwd4, sspmm_bwd_rows, ...): bytes
+Per kernel family (cbsr_stats4 = the fused pack + statistics, spgemm_fwd, pack_sel, sspmm_bwd4,
+sspmm_bwd_rows, ...): bytes
 per dispatch, dispatches per call (tools/pmc_driver.py makes 4 calls per direction), the
 average kernel duration of the same passes (kernel trace) and the resulting GB/s. Direction
 totals: "spgemm_fwd" = the forward kernel, "sspmm_bwd" = all SSpMM kernels of one backward
@@ -24,7 +26,8 @@ import re
 from collections import defaultdict
 
 CALLS = 4  # tools/pmc_driver.py: 1 + 3 calls per direction
-FWD = ("pack_cbsr_kernel", "pack_cbsr3_kernel", "zero_rows_kernel", "spgemm_fwd_kernel")
+FWD = ("cbsr_stats4_kernel", "cbsr_stats_kernel", "pack_cbsr3_kernel", "zero_rows_kernel",
+       "spgemm_fwd_kernel")
 BWD_PACK = ("pack_sel_kernel", "pack_sel2_kernel", "bwd_combine_kernel")  # per-call, beside the SSpMM
 
 
@@ -101,9 +104,26 @@ def main():
     ap.add_argument("--key", default="reddit:k16:d256:n1")
     ap.add_argument("--all", action="store_true",
                     help="root holds pmc_<dataset>_<kind>_k<k> directories")
+    ap.add_argument("--locality", action="store_true",
+                    help="root holds pmc_loc_<graph>_<order>_k<k> directories (tools/pmc_locality.sh)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
+    if args.locality:
+        out = os.path.join(os.path.dirname(args.out), "r03", "pmc_locality.json")
+        doc = {}
+        for d in sorted(glob.glob(os.path.join(args.root, "pmc_loc_*_k*"))):
+            ent = entry_for(d)
+            keep = {"lib_sha256": ent.get("lib_sha256")}
+            for fam in ("spgemm_fwd", "sspmm_bwd"):
+                det = ent.get(fam + "_detail", {})
+                keep[fam] = {x: det.get(x) for x in ("avg_ms", "ms_per_call", "bytes_per_dispatch",
+                                                      "l1_miss_requests", "l2_hit_rate", "GBps")
+                             if x in det}
+            doc[os.path.basename(d)[len("pmc_loc_"):]] = keep
+            print(os.path.basename(d), json.dumps(keep))
+        json.dump(doc, open(out, "w"), indent=1, sort_keys=True)
+        return
     doc = json.load(open(args.out)) if os.path.exists(args.out) else {}
     if args.all:
         for d in sorted(glob.glob(os.path.join(args.root, "pmc_*_k*"))):
