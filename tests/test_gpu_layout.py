@@ -240,7 +240,7 @@ def test_cbsr_stats_and_forward_ex_split(gpu):
     assert_close(b, ref, mag)
 
 
-@pytest.mark.parametrize("width", [30, 66, 7])
+@pytest.mark.parametrize("width", [30, 66, 7, 512, 1000])
 def test_dense_spmm_any_width(gpu, width):
     ptr, idx = graphs.synthetic_csr(2000, 40_000, seed=78)
     p, ix = ptr.numpy(), idx.numpy()
