@@ -250,8 +250,9 @@ def main():
         # the top-k lands in the shard's padded send buffers: the exchange copies nothing
         sp_data, sp_index = mk.maxk_forward(h, k, return_index=True, out=shard.local_buffers())
         plans = shard.plans
-        info = plans[0].info()
-        info["num_edges"] = sum(pl.info()["num_edges"] for pl in plans)
+        # the split keeps own / remote forward plans and one plan over all edges (last)
+        info = plans[-1].info()
+        info["num_edges"] = int(shard.ptr[-1])
         grad_sp = shard.grad_table
         shard.gather(sp_data, sp_index)
 
