@@ -1,6 +1,7 @@
 """Drives tools/ubench_vec.hip (tooling): time per wave64 gather instruction and per record
 ("edge") by load width and lanes per record, for an L2-resident (1 MB) and a 32 MB table.
-Run on the GPU box: python tools/ubench_vec.py"""
+Run on the GPU box: python tools/ubench_vec.py [table MB list, default 1,32; 0.015625 = 16 KB
+fits the 32 KB L1]"""
 import ctypes
 import json
 import os
@@ -23,8 +24,8 @@ PAT = [("16B x4 lanes (packed values)", 16, 4), ("4B x4 lanes at +64 (packed sel
        ("16B x2 lanes (32 B)", 16, 2), ("16B x1 lane", 16, 1), ("4B x1 lane", 4, 1),
        ("4B x16 lanes (64 B)", 4, 16), ("8B x4 lanes (32 B)", 8, 4), ("4B x4 lanes (16 B)", 4, 4)]
 out = torch.empty(NWG * 256, dtype=torch.int32, device=dev)
-for mb in (1, 32):
-    nrec = mb * 2**20 // 128
+for mb in [float(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,32").split(",")]:
+    nrec = int(mb * 2**20) // 128
     table = torch.randint(0, 2**31 - 1, (nrec * 32,), dtype=torch.int32, device=dev)
     for p, (name, by, lpe) in enumerate(PAT):
         ms = lib.ubench_vec(p, table.data_ptr(), nrec, out.data_ptr(), NWG, 5)
