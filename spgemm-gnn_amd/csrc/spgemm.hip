@@ -379,15 +379,41 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
 #pragma unroll
     for (int u = 0; u < U; ++u) wn[u] = load_cv(min(base + u * EPS + slot, last));
   }
+  // Edge-major windows (quad loads without prefetch, U % 4 == 0): sub-step u of slot s takes
+  // edge base + s U + u, so lane q of a quad loads the whole edge word of sub-step 4j + q
+  // (the quad reads 32 contiguous bytes) and DPP hands it to the quad: one edge-word
+  // instruction per four sub-steps instead of one per sub-step
+  // (Batching the selector words the same way, 64 scattered records per instruction, ran k = 16
+  // 1.10 -> 1.48 ms: only contiguous loads gain from fewer instructions.)
+  constexpr bool EM = QL && !PF && (U % 4) == 0;
   for (; base < e1; base += stride) {  // D: the accumulator's row stride
     uint32_t cw[U];
     float v[U];
     bool ok[U];
+    if constexpr (EM) {
+      const int qq = threadIdx.x & 3;
+      uint2 wq[U / 4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = base + u * EPS + slot;
-      ok[u] = lane_on && e < e1;
-      split_cv(PF ? wn[u] : load_cv(ok[u] ? e : last), cw[u], v[u]);
+      for (int j = 0; j < U / 4; ++j) wq[j] = cv[min(base + slot * U + 4 * j + qq, last)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = base + slot * U + u;
+        ok[u] = lane_on && e < e1;
+        const uint2 w = wq[u / 4];
+        switch (u & 3) {
+          case 0: cw[u] = quad_bcast<0>(w.x); v[u] = __uint_as_float(quad_bcast<0>(w.y)); break;
+          case 1: cw[u] = quad_bcast<1>(w.x); v[u] = __uint_as_float(quad_bcast<1>(w.y)); break;
+          case 2: cw[u] = quad_bcast<2>(w.x); v[u] = __uint_as_float(quad_bcast<2>(w.y)); break;
+          default: cw[u] = quad_bcast<3>(w.x); v[u] = __uint_as_float(quad_bcast<3>(w.y)); break;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = base + u * EPS + slot;
+        ok[u] = lane_on && e < e1;
+        split_cv(PF ? wn[u] : load_cv(ok[u] ? e : last), cw[u], v[u]);
+      }
     }
     float4 x[U];
     uint32_t sel[U];
@@ -817,23 +843,47 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + u * EPS + slot, t.e1 - 1));
   }
+  // Batched records (quad loads without prefetch, U % 4 == 0): lane q of a quad loads the
+  // whole record of its slot's edge in sub-step 4j + q (the wave's 64 loads cover 4 sub-steps'
+  // 64 consecutive records) and DPP hands each sub-step's record to the quad: one record
+  // instruction per four sub-steps. The sub-steps keep their consecutive edges (edges of a
+  // gather instruction share grad_out rows).
+  constexpr bool EM = Q && !PF && (U % 4) == 0;
   for (; base < t.e1; base += stride) {
     uint32_t go[U], cl[U];
     float v[U];
     bool ok[U];
+    if constexpr (EM) {
+      const int qq = lane & 3;
+      uint3 rq[U / 4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = base + u * EPS + slot;
-      ok[u] = lane_on && e < t.e1;
-      const uint3 r3 = PF ? rn[u] : load_rec(e);
-      if constexpr (Q) {
-        go[u] = quad_bcast<0>(r3.x);
-        cl[u] = quad_bcast<1>(r3.x);
-        v[u] = __uint_as_float(quad_bcast<2>(r3.x));
-      } else {
-        go[u] = r3.x;
-        cl[u] = r3.y;
-        v[u] = __uint_as_float(r3.z);
+      for (int j = 0; j < U / 4; ++j) rq[j] = rec3[base + (4 * j + qq) * EPS + slot];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ok[u] = lane_on && base + u * EPS + slot < t.e1;
+        const uint3 r3 = rq[u / 4];
+        switch (u & 3) {
+          case 0: go[u] = quad_bcast<0>(r3.x); cl[u] = quad_bcast<0>(r3.y); v[u] = __uint_as_float(quad_bcast<0>(r3.z)); break;
+          case 1: go[u] = quad_bcast<1>(r3.x); cl[u] = quad_bcast<1>(r3.y); v[u] = __uint_as_float(quad_bcast<1>(r3.z)); break;
+          case 2: go[u] = quad_bcast<2>(r3.x); cl[u] = quad_bcast<2>(r3.y); v[u] = __uint_as_float(quad_bcast<2>(r3.z)); break;
+          default: go[u] = quad_bcast<3>(r3.x); cl[u] = quad_bcast<3>(r3.y); v[u] = __uint_as_float(quad_bcast<3>(r3.z)); break;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = base + u * EPS + slot;
+        ok[u] = lane_on && e < t.e1;
+        const uint3 r3 = PF ? rn[u] : load_rec(e);
+        if constexpr (Q) {
+          go[u] = quad_bcast<0>(r3.x);
+          cl[u] = quad_bcast<1>(r3.x);
+          v[u] = __uint_as_float(quad_bcast<2>(r3.x));
+        } else {
+          go[u] = r3.x;
+          cl[u] = r3.y;
+          v[u] = __uint_as_float(r3.z);
+        }
       }
     }
     uint32_t s[U];
