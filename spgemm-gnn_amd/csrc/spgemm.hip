@@ -1328,12 +1328,34 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
   for (int base = e0; base < e1; base += EPS * U) {
     uint32_t c[U];
     float v[U];
+    if ((U & 3) == 0 && (L & 3) == 0) {
+      // lane q of a quad loads the record of sub-step 4j + q (contiguous), DPP hands it on:
+      // one record instruction per four sub-steps
+      const int qq = lane & 3;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = min(base + u * EPS + slot, e1 - 1);
-      const uint2 cv = *reinterpret_cast<const uint2*>(erec + 2 * (size_t)e);
-      c[u] = cv.x;  // column | (row % R) << kFwdColBits
-      v[u] = __uint_as_float(cv.y);
+      for (int j = 0; j < U / 4; ++j) {
+        const uint2 w = *reinterpret_cast<const uint2*>(
+            erec + 2 * (size_t)min(base + (4 * j + qq) * EPS + slot, e1 - 1));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int u = 4 * j + i;
+          if (u >= U) break;
+          switch (i) {
+            case 0: c[u] = quad_bcast<0>(w.x); v[u] = __uint_as_float(quad_bcast<0>(w.y)); break;
+            case 1: c[u] = quad_bcast<1>(w.x); v[u] = __uint_as_float(quad_bcast<1>(w.y)); break;
+            case 2: c[u] = quad_bcast<2>(w.x); v[u] = __uint_as_float(quad_bcast<2>(w.y)); break;
+            default: c[u] = quad_bcast<3>(w.x); v[u] = __uint_as_float(quad_bcast<3>(w.y)); break;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(base + u * EPS + slot, e1 - 1);
+        const uint2 cv = *reinterpret_cast<const uint2*>(erec + 2 * (size_t)e);
+        c[u] = cv.x;  // column | (row % R) << kFwdColBits
+        v[u] = __uint_as_float(cv.y);
+      }
     }
     uint32_t sw[U];
 #pragma unroll
@@ -1394,10 +1416,30 @@ __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int base = e0; base < e1; base += EPS * U) {
     int32_t pe[U];
+    if (!CS && (U & 3) == 0 && (L & 3) == 0) {
+      // lane q of a quad loads the permutation entry of sub-step 4j + q, DPP hands it on
+      const int qq = lane & 3;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = min(base + u * EPS + slot, e1 - 1);
-      pe[u] = CS ? j : (int32_t)(perm[j] - ebase);  // CS: the slots are already in column order
+      for (int jj = 0; jj < U / 4; ++jj) {
+        const uint32_t w = (uint32_t)(perm[min(base + (4 * jj + qq) * EPS + slot, e1 - 1)] - ebase);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int u = 4 * jj + i;
+          if (u >= U) break;
+          switch (i) {
+            case 0: pe[u] = (int32_t)quad_bcast<0>(w); break;
+            case 1: pe[u] = (int32_t)quad_bcast<1>(w); break;
+            case 2: pe[u] = (int32_t)quad_bcast<2>(w); break;
+            default: pe[u] = (int32_t)quad_bcast<3>(w); break;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = min(base + u * EPS + slot, e1 - 1);
+        pe[u] = CS ? j : (int32_t)(perm[j] - ebase);  // CS: the slots are already in column order
+      }
     }
     float4 t[U];
 #pragma unroll
