@@ -838,26 +838,40 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     if constexpr (Q) return make_uint3(recw[3 * (size_t)e], 0u, 0u);
     else return rec3[e];
   };
-  uint3 rn[U];
-  if (PF) {
+  constexpr bool EM = Q && (U % 4) == 0;
+  const int qq = lane & 3;
+  // EM: lane q of a quad loads sub-step 4j + q's whole record (records past e1 exist: padding)
+  auto load_rq = [&](int b, uint3 (&rq)[U / 4 > 0 ? U / 4 : 1]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + u * EPS + slot, t.e1 - 1));
+    for (int j = 0; j < U / 4; ++j) rq[j] = rec3[b + (4 * j + qq) * EPS + slot];
+  };
+  uint3 rn[U];
+  uint3 rqn[U / 4 > 0 ? U / 4 : 1];
+  if (PF) {
+    if constexpr (EM) {
+      load_rq(base, rqn);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + u * EPS + slot, t.e1 - 1));
+    }
   }
   // Batched records (quad loads without prefetch, U % 4 == 0): lane q of a quad loads the
   // whole record of its slot's edge in sub-step 4j + q (the wave's 64 loads cover 4 sub-steps'
   // 64 consecutive records) and DPP hands each sub-step's record to the quad: one record
   // instruction per four sub-steps. The sub-steps keep their consecutive edges (edges of a
   // gather instruction share grad_out rows).
-  constexpr bool EM = Q && !PF && (U % 4) == 0;
   for (; base < t.e1; base += stride) {
     uint32_t go[U], cl[U];
     float v[U];
     bool ok[U];
     if constexpr (EM) {
-      const int qq = lane & 3;
-      uint3 rq[U / 4];
+      uint3 rq[U / 4 > 0 ? U / 4 : 1];
+      if (PF) {
 #pragma unroll
-      for (int j = 0; j < U / 4; ++j) rq[j] = rec3[base + (4 * j + qq) * EPS + slot];
+        for (int j = 0; j < U / 4; ++j) rq[j] = rqn[j];
+      } else {
+        load_rq(base, rq);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         ok[u] = lane_on && base + u * EPS + slot < t.e1;
@@ -901,8 +915,12 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     if (PF) {  // unconditional (clamped): a branch here would make the updates below wait
                // for these loads too (vmcnt counts both paths)
       __builtin_amdgcn_sched_barrier(0);  // keep every gather ahead of these loads
+      if constexpr (EM) {
+        load_rq(base + stride, rqn);
+      } else {
 #pragma unroll
-      for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + stride + u * EPS + slot, t.e1 - 1));
+        for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + stride + u * EPS + slot, t.e1 - 1));
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
