@@ -17,6 +17,7 @@ messages for the same checks. Differences (all fixes of SURVEY §8(b) defects):
 from __future__ import annotations
 
 import collections
+import contextlib
 import ctypes
 import os
 import threading
@@ -35,6 +36,14 @@ def _stream() -> ctypes.c_void_p:
 
 def _p(t: Optional[torch.Tensor]) -> ctypes.c_void_p:
     return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+_SAME_DEVICE = contextlib.nullcontext()
+
+
+def _device(dev: torch.device):
+    """``torch.cuda.device(dev)``, or a no-op when ``dev`` is already current (host cost)."""
+    return _SAME_DEVICE if dev.index == torch.cuda.current_device() else torch.cuda.device(dev)
 
 
 def _need(cond: bool, msg: str) -> None:
@@ -87,7 +96,7 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
               sp_index.is_contiguous() and sp_index.device == input.device,
               "out[1] must be a contiguous uint8 [N, k] tensor on the input's device")
     count = torch.empty(n, dtype=torch.int32, device=input.device) if return_count else None
-    with torch.cuda.device(input.device):
+    with _device(input.device):
         check(lib.maxk_topk_cbsr_count(_p(input), _p(sp_data), _p(sp_index), _p(count), n, d,
                                        k, TOPK_MODES[mode], _stream()), "maxk_forward")
     res = (sp_data, sp_index) if return_index else (sp_data,)
@@ -121,7 +130,7 @@ def maxk_backward(grad_output: torch.Tensor, indices: torch.Tensor,
         dim_origin = int(indices.max().item()) + 1 if indices.numel() else 1
     _need(1 <= k <= dim_origin <= 256, "k must be between 1 and input dimension")
     grad_in = torch.empty((n, dim_origin), dtype=torch.float32, device=grad_output.device)
-    with torch.cuda.device(grad_output.device):
+    with _device(grad_output.device):
         check(lib.maxk_scatter_backward(_p(grad_output), _p(indices), _p(grad_in), n,
                                         dim_origin, k, _stream()), "maxk_backward")
     return grad_in
@@ -383,7 +392,8 @@ def spgemm_forward(ptr, idx, val, sp_data, sp_index, num_nodes: int, num_edges: 
     SO@0x221a0; checks bindings.cpp:45-54): ``out[r] = sum_nz val[nz] *
     densify(sp_data[idx[nz]], sp_index[idx[nz]])``.
     """
-    _check_graph(ptr, idx, val, num_nodes, num_edges)
+    if plan is None or plan._refs[0] is not ptr or plan._refs[1] is not idx or plan._refs[2] is not val:
+        _check_graph(ptr, idx, val, num_nodes, num_edges)  # (a plan's own tensors were checked)
     _check_tensor(sp_data, "sp_data", torch.float32)
     _check_tensor(sp_index, "sp_index", torch.uint8)
     _need(sp_data.shape == (num_nodes, dim_k) and sp_index.shape == (num_nodes, dim_k),
@@ -394,7 +404,7 @@ def spgemm_forward(ptr, idx, val, sp_data, sp_index, num_nodes: int, num_edges: 
     _need(plan.num_rows == num_nodes and plan.num_edges == num_edges and
           plan.dim_k == dim_k and plan.dim_origin == dim_origin,
           "plan was built for a different graph / k / D")
-    with torch.cuda.device(sp_data.device):
+    with _device(sp_data.device):
         out = plan.forward(sp_data, sp_index)
     return out, sp_index
 
@@ -408,7 +418,8 @@ def spgemm_backward(ptr, idx, val, grad_output, sp_index, num_nodes: int, num_ed
     num_edges, dim_k, dim_origin) -> [num_nodes, dim_k]`` (spgemm_backward_cuda
     SO@0x22490; checks bindings.cpp:65-71).
     """
-    _check_graph(ptr, idx, val, num_nodes, num_edges)
+    if plan is None or plan._refs[0] is not ptr or plan._refs[1] is not idx or plan._refs[2] is not val:
+        _check_graph(ptr, idx, val, num_nodes, num_edges)
     _check_tensor(grad_output, "grad_output", torch.float32)
     _check_tensor(sp_index, "sp_index", torch.uint8)
     _need(grad_output.shape == (num_nodes, dim_origin), "grad_output must be [num_nodes, dim_origin]")
@@ -419,7 +430,7 @@ def spgemm_backward(ptr, idx, val, grad_output, sp_index, num_nodes: int, num_ed
     _need(plan.num_rows == num_nodes and plan.num_edges == num_edges and
           plan.dim_k == dim_k and plan.dim_origin == dim_origin,
           "plan was built for a different graph / k / D")
-    with torch.cuda.device(grad_output.device):
+    with _device(grad_output.device):
         grad_sp = plan.backward(grad_output, sp_index)
     return grad_sp
 
