@@ -113,6 +113,19 @@ def test_topk_random_bit_exact(gpu, d, mode):
         assert np.array_equal(gd.cpu().numpy(), od), (d, k)
 
 
+@pytest.mark.parametrize("d,k", [(100, 5), (256, 64), (37, 37)])
+def test_topk_eight_rows_per_wave_bit_exact(gpu, d, k):
+    """N >= 2^20 rows takes the 8-rows-per-wave exact kernel (maxk_topk.hip kTopkRows8),
+    including a ragged last wave, odd k (byte-stored selectors) and k == D."""
+    n = (1 << 20) + 3
+    x = graphs.features(n, d, seed=k)
+    x[n - 1, :] = 0.25                              # tied row in the ragged last wave
+    gd, gi = mk.maxk_forward(x.to(gpu), k, mode="exact", return_index=True)
+    od, oi = oracle.maxk(x.numpy(), k, "exact")
+    assert np.array_equal(gi.cpu().numpy(), oi)
+    assert np.array_equal(gd.cpu().numpy(), od)
+
+
 def test_topk_default_returns_reference_shape(gpu):
     x = graphs.features(10, 64, seed=1).to(gpu)
     out = mk.maxk_forward(x, 16)
