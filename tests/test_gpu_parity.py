@@ -126,6 +126,50 @@ def test_topk_eight_rows_per_wave_bit_exact(gpu, d, k):
     assert np.array_equal(gd.cpu().numpy(), od)
 
 
+def _offset_view(t: torch.Tensor, gpu) -> torch.Tensor:
+    """A contiguous copy of ``t`` whose storage starts one element past an allocation
+    boundary (4-B misaligned floats/ints, odd byte address for u8)."""
+    buf = torch.empty(t.numel() + 1, dtype=t.dtype, device=gpu)
+    v = buf[1:].view(t.shape)
+    v.copy_(t.to(gpu))
+    assert v.is_contiguous() and v.data_ptr() % 16 != 0
+    return v
+
+
+@pytest.mark.parametrize("k", [8, 16, 32, 24])
+def test_offset_views_through_every_entry_point(gpu, k):
+    """Contiguous tensors need not be 16-B aligned (a view one element into a buffer): the
+    top-k, both aggregation directions (plan built from offset graph tensors too) and the
+    MaxK scatter give the aligned results."""
+    p, ix, v = GRAPHS["synthetic"]()
+    n, d = p.size - 1, 256
+    x = graphs.features(n, d, seed=k)
+    g = graphs.features(n, d, seed=k + 1)
+    od, oi = oracle.maxk(x.numpy(), k)
+    for mode in ("exact", "ref_compat"):
+        md, mi = oracle.maxk(x.numpy(), k, mode)
+        sd = _offset_view(torch.zeros(n, k), gpu)
+        si = _offset_view(torch.zeros(n, k, dtype=torch.uint8), gpu)
+        mk.maxk_forward(_offset_view(x, gpu), k, mode=mode, out=(sd, si))
+        assert np.array_equal(si.cpu().numpy(), mi), mode
+        assert np.array_equal(sd.cpu().numpy(), md), mode
+    ptr, idx, val = (_offset_view(torch.from_numpy(a), gpu) for a in (p, ix, v))
+    sd, si = _offset_view(torch.from_numpy(od), gpu), _offset_view(torch.from_numpy(oi), gpu)
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    out, _ = mk.spgemm_forward(ptr, idx, val, sd, si, n, ix.size, k, d)
+    assert_close(out, ref, mag)
+    ref, mag = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
+    gs = mk.spgemm_backward(ptr, idx, val, _offset_view(g, gpu), si, n, ix.size, k, d)
+    assert_close(gs, ref, mag)
+    gin = mk.maxk_backward(_offset_view(gs, gpu), si, dim_origin=d)
+    assert np.array_equal(gin.cpu().numpy(), oracle.maxk_backward(gs.cpu().numpy(), oi, d))
+    dense = oracle.maxk_backward(od, oi, d)  # densified CBSR rows
+    ref = oracle.dense_spmm(p, ix, v, dense)
+    mag = oracle.dense_spmm(p, ix, np.abs(v), np.abs(dense))
+    y = mk.dense_spmm(ptr, idx, val, _offset_view(torch.from_numpy(dense), gpu))
+    assert_close(y, ref, mag, rtol=2e-6 * 64)  # f32 sums in two orders (test_dense_spmm_vs_oracle)
+
+
 def test_topk_default_returns_reference_shape(gpu):
     x = graphs.features(10, 64, seed=1).to(gpu)
     out = mk.maxk_forward(x, 16)
