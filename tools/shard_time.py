@@ -47,6 +47,8 @@ def main():
                                           '{"split": false, "stats": false}, '
                                           '{"split": true, "stats": true}]')
     ap.add_argument("--opts", default="{}", help="plan options (JSON dict)")
+    ap.add_argument("--phases", default="1", help="column phases to try (comma list; > 1 "
+                    "drops the statistics row)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS[args.dataset]
@@ -58,8 +60,9 @@ def main():
     sd, si = mk.maxk_forward(h, k, return_index=True)
     del h
     opts = json.loads(args.opts)
-    for world in [int(w) for w in args.worlds.split(",")]:
-        part = RowPartition(ptr, world)
+    for world, phases in [(int(w), int(p)) for w in args.worlds.split(",")
+                          for p in args.phases.split(",")]:
+        part = RowPartition(ptr, world, phases=phases)
         for var in json.loads(args.variants):
             worst = 0.0
             for q in sorted({0, world - 1}):
@@ -83,11 +86,12 @@ def main():
                 tf = timeit(shard.compute_forward)
                 tb = timeit(lambda: shard.compute_backward(gl))
                 worst = max(worst, tf + tb)
-                print(json.dumps({"world": world, **var, "opts": opts, "rank": q,
+                print(json.dumps({"world": world, "phases": phases, **var, "opts": opts, "rank": q,
                                   "edges": int(shard.ptr[-1]), "fwd_ms": tf, "bwd_ms": tb,
                                   "plans": [p.info() for p in shard.plans]}), flush=True)
                 del shard
-            print(json.dumps({"world": world, **var, "opts": opts, "compute_ms_max": worst,
+            print(json.dumps({"world": world, "phases": phases, **var, "opts": opts,
+                              "compute_ms_max": worst,
                               "edges_per_s_compute_only": 2 * e / (worst * 1e-3)}), flush=True)
 
 
