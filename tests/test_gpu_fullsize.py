@@ -7,6 +7,7 @@ workload) and k=8/64, ogbn-products SAGE k=32, ogbn-proteins GCN k in {8,16,32,6
 * linearity          SpGEMM(2 sp_data) == 2 SpGEMM(sp_data)
 * sampled rows       forward rows vs the oracle on the induced sub-CSR
 * sampled columns    backward columns vs the oracle on the columns' in-edges
+* every row/column   the whole forward and backward outputs vs the oracle
 """
 import numpy as np
 import pytest
@@ -108,6 +109,31 @@ def test_sampled_columns_vs_oracle(case):
     np.add.at(mag, c, np.abs(terms))
     ok, worst = oracle.close_enough(gs.cpu().numpy()[cols], ref[cols], mag[cols])
     assert ok, worst
+
+
+def _close_in_chunks(got, ref, mag, rows=1 << 17):
+    worst = 0.0
+    for a in range(0, ref.shape[0], rows):
+        ok, w = oracle.close_enough(got[a:a + rows], ref[a:a + rows], mag[a:a + rows])
+        worst = max(worst, w)
+        assert ok, (a, w)
+    return worst
+
+
+def test_every_row_and_column_vs_oracle(case):
+    """The whole forward output and the whole backward output at config size against the
+    oracle's C/OpenMP restatement (f64 sums; the same bar as the small-graph parity tests)."""
+    ptr, idx, val, sp_data, sp_index, g, _, K = case
+    N, E = ptr.numel() - 1, idx.numel()
+    p, ix, v = ptr.cpu().numpy(), idx.cpu().numpy(), val.cpu().numpy()
+    si = sp_index.cpu().numpy()
+    y, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, N, E, K, D)
+    ref, mag = oracle.spgemm_forward(p, ix, v, sp_data.cpu().numpy(), si, D, with_mag=True)
+    print(f"forward: worst err/bound {_close_in_chunks(y.cpu().numpy(), ref, mag):.3g}")
+    del y, ref, mag
+    gs = mk.spgemm_backward(ptr, idx, val, g, sp_index, N, E, K, D)
+    ref, mag = oracle.sspmm_backward(p, ix, v, g.cpu().numpy(), si, with_mag=True)
+    print(f"backward: worst err/bound {_close_in_chunks(gs.cpu().numpy(), ref, mag):.3g}")
 
 
 # ------------------------------------------------------------------ top-k at config size
