@@ -42,6 +42,13 @@ constexpr double kFwdSlotEdgeRateFixed = 2.6e8;  // the same with the fixed-poin
 // even where two tables would otherwise be used (plan.hip: k >= 32 / k < 32)
 constexpr double kFwdPackedTableBytes = 150e6;
 constexpr double kFwdPackedTableBytes16 = 32e6;
+// k < 32: below kFwdPackMinEdgesPerCol edges per column the forward gathers from the two API
+// tables instead of packing one record per column per call; below kFwdPackMinEdgesPerColL2
+// too while the selector table (k bytes per column) stays L2-resident, where the second
+// (selector) touch of an edge is cheap (plan.hip)
+constexpr long long kFwdPackMinEdgesPerCol = 40;
+constexpr long long kFwdPackMinEdgesPerColL2 = 128;
+constexpr double kFwdSelL2Bytes = 3e6;
 // two-pass backward below this many expected edges per (row, column block), i.e. when a
 // column block sees each grad_out row it fetches about once. Measured (blocks vs two-pass,
 // ms): ogbn-products k = 16 (0.04) 13.4 / 6.0, k = 32 (0.02) 16.0 / 8.3; yelp k = 64 (0.015)

@@ -1068,19 +1068,27 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
 
   // Two tables (no record pack): Reddit k = 32 2.65 -> 2.53 ms, k = 64 4.98 -> 4.92 (k = 16:
   // 1.35 vs 1.39 packed); and where the per-call pack of all NC records costs more than it
-  // saves, below ~128 edges per column (an 8-GPU row shard of Reddit at k = 16: 0.221 ->
-  // 0.207 ms). But on a large table, whose gathers mostly miss L2, the record's one line
+  // saves: below kFwdPackMinEdgesPerCol edges per column, or below kFwdPackMinEdgesPerColL2
+  // with an L2-resident selector table (round 3, the pack fused into the statistics pass;
+  // per-rank forward on row shards at k = 16: Reddit W = 8, 62 edges per column and a 3.7 MB
+  // selector table, 0.172 ms packed vs 0.183 two tables, W = 4 (123) 0.757 vs 0.805 ms for
+  // the rank's whole step; ogbn-proteins W = 8, 75 edges per column and 2.1 MB of selectors,
+  // 0.144 packed vs 0.138 two tables; round 2 with a separate pack: Reddit W = 8 0.221
+  // packed vs 0.207). But on a large table, whose gathers mostly miss L2, the record's one line
   // beats the two tables' two (values + selectors): at k = 16 from tens of MB (yelp, 57 MB:
-  // 0.645 -> 0.54 ms packed; ogbn-products, 196 MB: 4.84 -> 2.95; flickr 7 MB and the
-  // Reddit shard 19 MB stay faster with two tables), at k = 32 only from HBM-sized tables
+  // 0.645 -> 0.54 ms packed; ogbn-products, 196 MB: 4.84 -> 2.95; flickr, 7 MB at 11 edges
+  // per column, stays faster with two tables), at k = 32 only from HBM-sized tables
   // (ogbn-products 392 MB: 4.95 -> 4.77; yelp 115 MB: 0.67 two tables vs 0.73); never at
   // k = 64 (ogbn-products 7.08 two tables vs 7.44)
   const bool big_table = (double)std::max(NC, 1) * 5.0 * k >
                          (k >= 32 ? kFwdPackedTableBytes : kFwdPackedTableBytes16);
+  const bool sel_l2 = (double)std::max(NC, 1) * k <= kFwdSelL2Bytes;
+  const bool few_edges = E < kFwdPackMinEdgesPerCol * std::max(NC, 1) ||
+                         (sel_l2 && E < kFwdPackMinEdgesPerColL2 * std::max(NC, 1));
   p->fwd_two_tables = !p->fwd_chunk3 && k % 4 == 0 &&
                       (o.fwd_two_tables == 1 ||
                        (o.fwd_two_tables == 0 &&
-                        (k >= 64 || (!big_table && (k >= 32 || E < 128ll * std::max(NC, 1))))));
+                        (k >= 64 || (!big_table && (k >= 32 || few_edges)))));
   if (p->fwd_two_tables) {
     // no workspace: the kernel gathers from sp_data / sp_index
   } else if (p->fwd_chunk3 && NC > 0) {

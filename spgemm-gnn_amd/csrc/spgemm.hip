@@ -148,8 +148,14 @@ __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restric
                                                           const uint8_t* __restrict__ sel,
                                                           int64_t nrows, int k, uint32_t* st0,
                                                           uint32_t* st1, uint8_t* __restrict__ rec,
-                                                          int rec_bytes) {
+                                                          int rec_bytes,
+                                                          const int32_t* __restrict__ zrows,
+                                                          int nz, float* __restrict__ out, int D) {
   __shared__ uint32_t smx[256 / kWave], smn[256 / kWave];
+  // the forward's split rows (summed atomically by their segments) start from zero: zeroed
+  // here, one launch before the forward, instead of by a zero_rows_kernel launch of their own
+  for (int i = blockIdx.x; i < nz; i += gridDim.x)
+    for (int t = threadIdx.x; t < D; t += blockDim.x) out[(size_t)zrows[i] * D + t] = 0.f;
   const int L = k >> 2;
   const int RW = kWave / L;  // rows per wave
   const int lane = threadIdx.x & (kWave - 1);
@@ -1572,9 +1578,12 @@ using namespace maxk;
 // for k % 4 == 0 (~10 us for Reddit at k = 16), one thread per row otherwise.
 // rec != nullptr (k % 4 == 0 only): also pack the forward's CBSR records (st0 == nullptr: the
 // pack alone)
+// zrows/nz/out/D (k % 4 == 0 only): split rows of the forward to zero in the same launch.
 static int launch_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int64_t nrows, int k,
                              uint32_t* st0, uint32_t* st1, int cus, hipStream_t s,
-                             uint8_t* rec = nullptr, int rec_bytes = 0) {
+                             uint8_t* rec = nullptr, int rec_bytes = 0,
+                             const int32_t* zrows = nullptr, int nz = 0, float* out = nullptr,
+                             int D = 0) {
   if (nrows <= 0) return MAXK_OK;
   if (k % 4 == 0) {
     const int64_t rows_per_block = (256 / kWave) * (kWave / (k / 4));
@@ -1585,13 +1594,13 @@ static int launch_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int6
         1, std::min<int64_t>((nrows + rows_per_block - 1) / rows_per_block, cap));
     if (rec && st0)
       hipLaunchKernelGGL((cbsr_stats4_kernel<true, true>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes);
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D);
     else if (rec)
       hipLaunchKernelGGL((cbsr_stats4_kernel<true, false>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes);
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D);
     else
       hipLaunchKernelGGL((cbsr_stats4_kernel<false, true>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes);
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D);
   } else {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nrows + 255) / 256, 2 * cus));
     hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nrows,
@@ -1643,11 +1652,9 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   }
   hipStream_t s = (hipStream_t)stream;
   uint8_t* rec_ws = ws_base;
-  if (plan->n_zero_rows > 0 && !accum) {  // split rows are summed atomically into zeroed rows
-    hipLaunchKernelGGL(zero_rows_kernel, dim3(plan->n_zero_rows), dim3(256), 0, s,
-                       plan->zero_rows, plan->n_zero_rows, out, D);
-    MAXK_LAUNCH_CHECK("zero_rows launch");
-  }
+  // split rows are summed atomically into zeroed rows: zeroed by the statistics / pack launch
+  // when there is one (k % 4 == 0), else by a launch of their own
+  const int nz = accum ? 0 : plan->n_zero_rows;
   const int R = plan->fwd_tile_rows;
   const int B = plan->fwd_phases;
   const size_t lds = fwd_lds_bytes(R, D, plan->fwd_acc);
@@ -1685,10 +1692,16 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
                        rec_ws, plan->num_cols, k, rec_bytes);
     MAXK_LAUNCH_CHECK("pack_cbsr3 launch");
   }
+  const bool zero_in_stats = (pack4 || st) && k % 4 == 0;
+  if (nz > 0 && !zero_in_stats) {
+    hipLaunchKernelGGL(zero_rows_kernel, dim3(nz), dim3(256), 0, s, plan->zero_rows, nz, out, D);
+    MAXK_LAUNCH_CHECK("zero_rows launch");
+  }
   if (pack4 || st) {
     const int rc = launch_cbsr_stats(sp_data, sp_index, plan->num_cols, k, st,
                                      st ? st + 32 : nullptr, plan->cus, s,
-                                     pack4 ? rec_ws : nullptr, rec_bytes);
+                                     pack4 ? rec_ws : nullptr, rec_bytes, plan->zero_rows,
+                                     zero_in_stats ? nz : 0, out, D);
     if (rc) return rc;
   }
   const int rot = plan->fwd_rot_ticks;
