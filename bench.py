@@ -51,8 +51,9 @@ def bwd_bytes(n, e, k, d):
 
 
 def log(*a):
-    if int(os.environ.get("RANK", "0")) == 0:
-        print(*a, file=sys.stderr, flush=True)
+    # MAXK_BENCH_VERBOSE=1: every rank logs (multi-rank rehearsals)
+    if int(os.environ.get("RANK", "0")) == 0 or os.environ.get("MAXK_BENCH_VERBOSE"):
+        print(f"[rank {os.environ.get('RANK', '0')}]", *a, file=sys.stderr, flush=True)
 
 
 def event_time_ms(fn, reps):
@@ -152,6 +153,9 @@ def cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d, sample_frac, reps, log_
 
 
 def main():
+    if os.environ.get("MAXK_BENCH_TRACEBACK_S"):  # where a stuck rank is (rehearsals)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["MAXK_BENCH_TRACEBACK_S"]), repeat=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -197,6 +201,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        log(f"process group up ({backend}, world {world})")
 
     n, e_target = graphs.DATASETS[args.dataset]
     d, k = args.dim, args.k
@@ -272,6 +277,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    log("warm-up done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
