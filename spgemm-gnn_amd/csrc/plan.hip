@@ -945,8 +945,14 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     const int nt = (int)ftasks.size();
     std::vector<int32_t> order(nt);
     for (int i = 0; i < nt; ++i) order[i] = i;
-    std::sort(order.begin(), order.end(),
-              [&](int a, int b) { return ftasks[a].e0 < ftasks[b].e0; });
+    // by first edge, and among equal first edges the empty tasks (an edgeless tile shares its
+    // e0 with the next tile) before the one task that owns edges there: fwd_key_kernel takes
+    // the LAST task whose first edge is <= e (an edgeless tile ordered last took the next
+    // tile's edges, whose rows then stayed zero: tests/test_gpu_fuzz.py)
+    std::sort(order.begin(), order.end(), [&](int a, int b) {
+      if (ftasks[a].e0 != ftasks[b].e0) return ftasks[a].e0 < ftasks[b].e0;
+      return ftasks[a].e1 < ftasks[b].e1;
+    });
     std::vector<int32_t> starts(nt), ranks(nt), row0s(nt);
     for (int i = 0; i < nt; ++i) {
       starts[i] = ftasks[order[i]].e0;

@@ -237,6 +237,25 @@ def test_spgemm_forward_vs_oracle(gpu, gname, d, k):
     assert_close(out, ref, mag)
 
 
+@pytest.mark.parametrize("n,row", [(48, 47), (48, 32), (33, 32), (64, 63), (100, 70)])
+@pytest.mark.parametrize("d,k", [(1, 1), (256, 16), (256, 8), (256, 32)])
+def test_spgemm_forward_edgeless_tiles_before_edges(gpu, n, row, d, k):
+    """Every row before `row` is edgeless, so whole forward tiles share their (empty) first
+    edge with the tile that owns the edges; the edges must still land in `row` (found by
+    tests/test_gpu_fuzz.py: a tile ordered after its edgeless neighbour lost its edges)."""
+    rs = np.random.RandomState(n + row)
+    p = np.zeros(n + 1, np.int32)
+    p[row + 1:] = min(n, 40)
+    ix = np.sort(rs.choice(n, min(n, 40), replace=False)).astype(np.int32)
+    v = rs.randn(ix.size).astype(np.float32)
+    x = graphs.features(n, d, seed=k)
+    od, oi = oracle.maxk(x.numpy(), k)
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    out, _ = mk.spgemm_forward(ptr, idx, val, to_dev(od, gpu), to_dev(oi, gpu), n, ix.size, k, d)
+    assert_close(out, ref, mag)
+
+
 def test_spgemm_forward_duplicate_selectors_summed(gpu):
     p = np.array([0, 2, 3], np.int32)
     ix = np.array([0, 1, 1], np.int32)
