@@ -37,7 +37,7 @@ def _graph(rs, n, avg_deg, heavy, unsorted, repeats):
     return ptr, idx, val
 
 
-@settings(max_examples=60, deadline=None, derandomize=True,
+@settings(max_examples=150, deadline=None, derandomize=True,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(n=st.integers(1, 2500), avg_deg=st.sampled_from([0.0, 0.5, 3.0, 20.0, 60.0]),
        d=st.integers(1, 256), kfrac=st.floats(0.0, 1.0), heavy=st.booleans(),
