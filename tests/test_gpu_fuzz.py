@@ -9,7 +9,7 @@ MaxK scatter exactly.
 import numpy as np
 import pytest
 import torch
-from hypothesis import HealthCheck, given, settings
+from hypothesis import HealthCheck, assume, given, settings
 from hypothesis import strategies as st
 
 import maxk_kernels as mk
@@ -68,3 +68,36 @@ def test_random_graph_vs_oracle(gpu, n, avg_deg, d, kfrac, heavy, unsorted, repe
     gin = mk.maxk_backward(gs, si, dim_origin=d)
     assert np.array_equal(gin.cpu().numpy(), oracle.maxk_backward(gs.cpu().numpy(), oi, d))
     mk.clear_plan_cache()
+
+
+@settings(max_examples=100, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture,
+                                 HealthCheck.filter_too_much])
+@given(n=st.integers(1, 1500), avg_deg=st.sampled_from([0.0, 0.5, 3.0, 20.0, 60.0]),
+       d=st.integers(1, 256), kfrac=st.floats(0.0, 1.0), heavy=st.booleans(),
+       opt=st.integers(0, 10_000), seed=st.integers(0, 2**31 - 1))
+def test_random_graph_plan_options_vs_oracle(gpu, n, avg_deg, d, kfrac, heavy, opt, seed):
+    """The same draws through a plan built with one of the parity tests' option sets
+    (tests/test_gpu_parity.py PLAN_OPTIONS); option sets a (k, D) does not support are
+    rejected at plan creation and skipped."""
+    from test_gpu_parity import PLAN_OPTIONS
+    opts = PLAN_OPTIONS[opt % len(PLAN_OPTIONS)]
+    rs = np.random.RandomState(seed)
+    k = max(1, min(d, int(round(kfrac * d))))
+    p, ix, v = _graph(rs, n, avg_deg, heavy, unsorted=bool(seed & 1), repeats=bool(seed & 2))
+    x = rs.randn(n, d).astype(np.float32)
+    g = rs.randn(n, d).astype(np.float32)
+    od, oi = oracle.maxk(x, k, "exact")
+    ptr, idx, val = (torch.from_numpy(a).to(gpu) for a in (p, ix, v))
+    try:
+        plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k, options=opts)
+    except RuntimeError:
+        assume(False)
+    out = plan.forward(torch.from_numpy(od).to(gpu), torch.from_numpy(oi).to(gpu))
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    ok, worst = oracle.close_enough(out.cpu().numpy(), ref, mag)
+    assert ok, ("forward", opts, worst)
+    gs = plan.backward(torch.from_numpy(g).to(gpu), torch.from_numpy(oi).to(gpu))
+    ref, mag = oracle.sspmm_backward(p, ix, v, g, oi, with_mag=True)
+    ok, worst = oracle.close_enough(gs.cpu().numpy(), ref, mag)
+    assert ok, ("backward", opts, worst)
