@@ -10,8 +10,9 @@ value = 2E / step time (edges/s = 2E / (t_fwd + t_bwd)).
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
 
 N > 1: the rows are partitioned over the ranks (strong scaling: the Reddit graph is fixed)
-and each step includes the RCCL all-gather of the CBSR block and the reduce-scatter of
-grad_sp (maxk_kernels.dist). Rank 0 prints one JSON line.
+and each step includes the RCCL all-gather of the CBSR records and the reduce-scatter of
+grad_sp (maxk_kernels.dist). Each rank generates only its own rows of the graph (counter-based
+draws: every N benchmarks the same graph). Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -162,13 +163,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--dataset", default="reddit", choices=sorted(graphs.DATASETS))
     ap.add_argument("--k", type=int, default=16)
-    ap.add_argument("--phases", type=int, default=1,
-                    help="column phases of the N > 1 exchange (all-gather / reduce-scatter of "
-                         "one phase overlapping the other's compute; 1 = one-shot, the default: "
-                         "2 phases cost +14 %% per-rank compute at W=8, tools/shard_time.py)")
-    ap.add_argument("--split", action="store_true",
-                    help="N > 1: local-columns-first split of the forward (own-column edges "
-                         "computed while the all-gather is in flight; maxk_kernels.dist)")
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--cpu-sample", type=float, default=1.0,
                     help="fraction of E timed per direction for the CPU baseline")
@@ -205,30 +199,57 @@ def main():
 
     n, e_target = graphs.DATASETS[args.dataset]
     d, k = args.dim, args.k
-    t0 = time.perf_counter()
+    # ranks that share a device (a gloo rehearsal on a one-GPU box) take turns through the
+    # setup: four processes' radix sorts at once on one GPU stalled for minutes
+    shared = world > 1 and backend == "gloo" and world > torch.cuda.device_count()
+
+    def setup_turns(fn):
+        if not shared:
+            return fn()
+        res = None
+        for q in range(world):
+            if q == rank:
+                res = fn()
+                torch.cuda.synchronize()
+            dist.barrier()
+        return res
+
     gpath = None
     if args.graph == "auto":
         gpath = graphs.find_dgl_graph(args.dataset)
     elif args.graph != "synthetic":
         gpath = args.graph
-    if gpath:
-        ptr, idx = graphs.load_npz_csr(gpath, device=dev)
-        n = ptr.numel() - 1
-        data = (f"graph loaded from {gpath} (+ self-loops); N(0,1) features seed 97, "
-                f"upstream grad seed 98")
-    else:
-        ptr, idx = graphs.synthetic_csr(n, e_target, seed=97, device=dev)
-        data = (f"synthetic ({args.dataset}-shaped graph: lognormal degrees sigma=1.2, uniform "
-                f"columns, self-loops, seed 97; N(0,1) features seed 97, upstream grad seed 98)")
-    val = graphs.sage_mean_values(ptr)
-    e = idx.numel()
-    torch.cuda.synchronize()
-    log(f"graph {args.dataset}: N={n} E={e} {'loaded' if gpath else 'generated'} in "
-        f"{time.perf_counter() - t0:.1f}s")
+
+    def build_graph():
+        t0 = time.perf_counter()
+        if gpath:
+            ptr, idx = graphs.load_npz_csr(gpath, device=dev)
+            data = (f"graph loaded from {gpath} (+ self-loops); N(0,1) features seed 97, "
+                    f"upstream grad seed 98")
+            part = RowPartition(ptr, world)
+            e0, e1 = part.edges(ptr, rank)
+            idx = idx[e0:e1].contiguous()
+        else:
+            ptr = graphs.synthetic_ptr(n, e_target, seed=97, device=dev)
+            part = RowPartition(ptr, world)
+            idx = graphs.synthetic_rows(ptr, seed=97, rows=part.rows(rank))
+            data = (f"synthetic ({args.dataset}-shaped graph: lognormal degrees sigma=1.2, "
+                    f"uniform columns from a counter-based stream, self-loops, seed 97; each "
+                    f"rank generates its own rows; N(0,1) features seed 97, upstream grad seed 98)")
+        r0, r1 = part.rows(rank)
+        lptr = ptr[r0:r1 + 1]
+        val = graphs.sage_mean_values(lptr, num_edges=idx.numel())   # the rank's edges
+        torch.cuda.synchronize()
+        log(f"graph {args.dataset}: rows [{r0}, {r1}) of N={ptr.numel() - 1}, "
+            f"{idx.numel()} edges {'loaded' if gpath else 'generated'} in "
+            f"{time.perf_counter() - t0:.1f}s")
+        return ptr, idx, val, part, data
+
+    ptr, idx, val, part, data = setup_turns(build_graph)
+    n = ptr.numel() - 1
+    e = int(part.num_edges)
     # PMC traffic in --traffic-json was collected on the synthetic graphs
     tkey = args.dataset if not gpath else args.dataset + ":file"
-
-    part = RowPartition(ptr, world, phases=args.phases if world > 1 else 1)
     r0, r1 = part.rows(rank)
     h = graphs.features(n, d, seed=97, device=dev)[r0:r1].contiguous()
     g = graphs.features(n, d, seed=98, device=dev)[r0:r1].contiguous()
@@ -251,17 +272,18 @@ def main():
             fwd()
             bwd()
     else:
-        shard = ShardedAggregation(part, rank, ptr, idx, val, d, k, split=args.split)
-        # the top-k lands in the shard's padded send buffers: the exchange copies nothing
-        sp_data, sp_index = mk.maxk_forward(h, k, return_index=True, out=shard.local_buffers())
-        plans = shard.plans
-        # the split keeps own / remote forward plans and one plan over all edges (last)
-        info = plans[-1].info()
-        info["num_edges"] = int(shard.ptr[-1])
+        def build_shard():
+            sh = ShardedAggregation(part, rank, ptr, idx, val, d, k, local_edges=True)
+            # the top-k lands in the shard's send records: the exchange copies nothing
+            bufs = mk.maxk_forward(h, k, return_index=True, out=sh.local_buffers())
+            return sh, bufs
+
+        shard, (sp_data, sp_index) = setup_turns(build_shard)
+        info = shard.plan.info()
         grad_sp = shard.grad_table
         shard.gather(sp_data, sp_index)
 
-        def fwd():  # this rank's kernels alone (all parts), no collectives
+        def fwd():  # this rank's kernels alone, no collectives
             shard.compute_forward()
 
         def bwd():
@@ -320,7 +342,7 @@ def main():
         tx = torch.tensor([ag_ms, rs_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tx, op=dist.ReduceOp.MAX)
         ag_ms, rs_ms = (float(v) for v in tx.tolist())
-        ag_bytes = 5 * k * part.padded_rows            # received table incl. own slice
+        ag_bytes = shard.table_rec.numel()             # received records incl. own slice
         rs_bytes = 4 * k * part.padded_rows            # grad_sp reduced over all columns
         exchange = {"all_gather_ms": ag_ms, "reduce_scatter_ms": rs_ms,
                     "all_gather_bytes": ag_bytes, "reduce_scatter_bytes": rs_bytes,
@@ -374,8 +396,7 @@ def main():
             "dim_k": k,
             "parallelism": "single-gpu" if world == 1 else
             f"row-partition x{world} + {'RCCL' if backend == 'nccl' else 'gloo (rehearsal)'} "
-            f"all-gather(CBSR) / reduce-scatter(grad_sp)"
-            + (", local-columns-first split" if args.split else ""),
+            f"all-gather(CBSR records) / reduce-scatter(grad_sp)",
         },
         "roofline": {
             "bound": "hbm",

@@ -21,19 +21,14 @@ constexpr int kFwdRowPad = 1;
 // forward edge word: source column in the low kFwdColBits bits, row within the tile above
 constexpr int kFwdColBits = 26;
 constexpr uint32_t kFwdColMask = (1u << kFwdColBits) - 1;
-constexpr int kFwdThreads = 256;        // 4 waves
-constexpr int kBwdThreads = 512;        // 8 waves
+constexpr int kFwdThreads = 256;        // 4 waves per forward work-group
+constexpr int kBwdThreads = 512;        // 8 waves per backward work-group (12 at k >= 32)
 constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
 constexpr int kFwdUnroll = 8;           // independent sub-steps in flight per wave
-constexpr int kBwdUnroll = 8;
-constexpr int kFwdWaves = 4;            // default wavefronts per forward work-group
-constexpr int kBwdWaves = 8;            // default wavefronts per backward work-group
-constexpr int kFwdFlagPrefetch = 1;     // forward kernel flags (template FL)
-constexpr int kFwdFlagBranchless = 2;
-constexpr int kFwdFlagChunk3 = 4;
-constexpr int kFwdFlagQuad = 8;
+constexpr int kFwdFlagChunk3 = 1;       // forward kernel flags (template FL): lane-chunk records
+constexpr int kFwdFlagQuad = 2;         // quad-shared edge-word loads
 constexpr int kBwdTasksPerCu = 2;
-constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k atomics) vs its edges
+constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k stores) vs its edges
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
 constexpr double kFwdSlotEdgeRate = 1.6e8;  // edges/s one forward slot sustains at k = 16
@@ -61,22 +56,15 @@ constexpr int kBwdRowsPerWave = 4;  // row pass: most destination rows one wavef
 // (ogbn-products k = 32, 15.8 GB in one chunk: 1 / 2 / 4 / 8 chunks ran 8.11 / 8.68 / 10.49 /
 // 14.60 ms; every chunk's column pass visits every column)
 constexpr double kBwdTwoPassWorkspaceCap = 16.0 * (1ull << 30);
-// cost-balanced backward chunks: a (column block, destination row) pair costs this many
-// quarter-edges on top of its edges (its grad_out lines are fetched once per pair). Measured
-// on the Reddit-size 41-community graph in ID order (ascending rows), k = 16: 1, 4, 8, 16, 24
-// quarter-edges ran 2.13, 2.03, 1.95, 2.07, 2.30 ms (equal edges 2.19); uniform graphs are
-// within +-0.3 % of equal edges at every value
-constexpr int kBwdRowCost4 = 8;
 // work-groups per CU of the fused CBSR pack + statistics pass (each adds one atomic per
 // statistics word, and same-address atomics serialise at the L2). Reddit, pack+stats at
 // k = 16 / stats at k = 32, 64: 1 -> 24.5 / 54.5 us, 4 -> 20.8 / 26.6 us, 8 -> 31.5 / 33.7 us
 // (the separate pack + stats passes took 21 + 17 us at k = 16)
 constexpr int kStatsBlocksPerCu = 4;
-constexpr int kBwdSlotGroups = 1;  // default S of the packed backward (plan: 2 at k >= 32 with
-                                     // few edges per block row)
-// Records past the end of the backward edge list that a wave may read (and ignore).
-constexpr int kBwdRecPad = (kBwdThreads / kWave) * kWave * 16 + kWave;  // MI355X: 8 XCDs, work-groups dealt round-robin (speed only)
-constexpr int kBwdLdsBudget = 160 * 1024; // all of a CU's LDS: one 512-thread work-group per CU
+// Records past the end of the backward edge list that a wave may read (and ignore): one
+// iteration of a wave covers at most 16 sub-steps x 64 edges.
+constexpr int kBwdRecPad = 16 * kWave + kWave;
+constexpr int kBwdLdsBudget = 160 * 1024; // all of a CU's LDS: one work-group per CU
 
 // Thread-local error message plumbing for maxk_last_error().
 void set_error(const std::string& msg);
@@ -144,12 +132,6 @@ struct BwdTask {
 };
 static_assert(sizeof(BwdTask) == 32, "BwdTask is 2 x dwordx4");
 
-__device__ __forceinline__ void lds_add(float* p, float v) {
-  // Lowers to ds_add_f32 (no return) for an LDS address. NOTE: ~30x slower than integer
-  // LDS atomics on gfx950 (tools/ubench_atomics); kept off the hot paths.
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 __device__ __forceinline__ void lds_add(double* p, double v) {
   // ds_add_f64 (no return).
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -172,11 +154,10 @@ struct maxk_plan {
   const int32_t* src_ptr = nullptr;  // identity of the graph the plan was built for
   const int32_t* src_idx = nullptr;
   int32_t cus = 256;             // compute units of the device the plan was built on
-  // forward
-  int32_t fwd_tile_rows = 16;
-  int32_t fwd_acc = MAXK_ACC_F64;
-  int32_t fwd_rec_bytes = 0;     // packed CBSR record size (k % 4 == 0)
-  uint8_t* fwd_rec = nullptr;    // [num_cols][fwd_rec_bytes] workspace (per call pack)
+  // ---- forward: tiles of whole rows (FwdTask), edges column-sorted per tile
+  int32_t fwd_tile_rows = 32;
+  int32_t fwd_rec_bytes = 0;     // packed CBSR record size (per-call pack)
+  uint8_t* fwd_rec = nullptr;    // [num_cols][fwd_rec_bytes] plan-owned workspace
   // fixed-point forward (LdsFix): per task {sexp, gexp} (fwd_fix_stats_kernel); the call's
   // {max |x|, min |x|} words live at fwd_xstat_off of the forward workspace
   int32_t fwd_fixed = 0;
@@ -184,58 +165,44 @@ struct maxk_plan {
   int32_t* fwd_rowptr = nullptr;  // plan copy of ptr for the bounds' row sums
   int64_t fwd_xstat_off = 0;
   maxk::FwdTask* fwd_tasks = nullptr;   // e0/e1 index the permuted edge order below
-  int32_t fwd_phases = 1;        // column phases per forward call
-  int32_t fwd_persistent = 0;    // grid = resident capacity (1) or one work-group per task
+  int32_t fwd_phases = 1;        // column windows of the rotated sweep (1: no rotation)
   int32_t fwd_rot_ticks = 0;     // > 0: rotated sweeps, s_memrealtime ticks per window
-  int32_t fwd_unroll = 8;        // independent sub-steps per wave (8 or 16)
-  int32_t bwd_unroll = 8;
-  int32_t fwd_waves = 4;         // wavefronts per forward work-group
-  int32_t bwd_waves = 8;         // wavefronts per backward work-group
-  int32_t fwd_prefetch = 0;      // next sub-steps' edge words loaded during the gathers
-  int32_t fwd_branchless = 1;    // idle lanes add 0 instead of branching around the update
   int32_t fwd_chunk3 = 0;        // lane-chunk records: 3 values + their selectors per 16 B
-  int32_t bwd_prefetch = 0;
-  int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per phase
+  int32_t fwd_quad = 0;          // quad-shared edge-word loads
+  int32_t fwd_two_tables = 0;    // gather from sp_data / sp_index directly (no pack)
+  int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per window
   int32_t* fwd_perm = nullptr;   // CSR edge id of each permuted forward edge
   uint2* fwd_cv = nullptr;       // {column | (row within the task << kFwdColBits), val bits}
   int32_t n_fwd_tasks = 0;
   int32_t* zero_rows = nullptr;  // rows written by split tasks (atomic), zeroed first
   int32_t n_zero_rows = 0;
-  // backward
-  int32_t bwd_acc = MAXK_ACC_F64;
-  int32_t bwd_feats = 1;         // features per lane (4: k/4 lanes per edge; 1: k lanes)
+  // ---- backward, column blocks (sspmm_bwd4_kernel): one 12-B record per reordered edge
+  // {row * D * 4 (or the row index when grad_out exceeds 4 GiB), column within its block,
+  // val}; F selector slots per lane, S slot groups, k padded to bwd_kp (a multiple of F * S;
+  // the padding slots gather feature 0 into accumulators that are never stored)
+  int32_t bwd_feats = 4;         // F: 4 or 2
+  int32_t bwd_slot_groups = 1;   // S
+  int32_t bwd_kp = 0;            // padded slots per column
+  int32_t bwd_ks = 0;            // accumulator floats per column and group (= bwd_kp / S)
+  int32_t bwd_unroll = 8;
+  int32_t bwd_waves = 8;
+  int32_t bwd_big = 0;           // grad_out > 4 GiB: 64-bit row addressing
   int32_t bwd_block_cols = 0;
   int32_t n_bwd_blocks = 0;
   maxk::BwdTask* bwd_tasks = nullptr;
   int32_t n_bwd_tasks = 0;
   int32_t n_bwd_shared = 0;
   int32_t* bwd_perm = nullptr;   // CSR edge id of each reordered edge
-  int32_t* bwd_row = nullptr;    // destination row r of each reordered edge
-  int32_t* bwd_col = nullptr;    // source column c
-  float* bwd_val = nullptr;      // val snapshot
-  // packed backward path (k % 4 == 0, f32 CAS accumulators, grad_out < 4 GiB): one 12-B
-  // record per reordered edge {row * D * 4, column within its block, val} replaces
-  // bwd_row/bwd_col/bwd_val, and a per-call selector table in lane order
   uint32_t* bwd_rec = nullptr;   // [num_edges + kBwdRecPad][3]
-  uint32_t* bwd_sel = nullptr;   // [S][num_cols][k / 4S] workspace: 4 selectors per lane
-  int32_t bwd_slot_groups = 1;   // S
-  int32_t bwd_ks = 0;            // accumulator floats per column (k/S + 1, or k/S unpadded)
-  int32_t bwd_sel_lds = 0;       // selector words of the block staged in LDS
-  int32_t bwd_cas64 = 0;         // 64-bit CAS pairs on adjacent slots (packed kernel)
-  int32_t bwd_quad = 0;          // quad-shared record loads (one dword per lane + DPP)
-  int32_t fwd_quad = 0;          // quad-shared edge-word loads
-  int32_t fwd_two_tables = 0;    // gather from sp_data / sp_index directly (no pack)
-  int32_t bwd_csc = 0;           // column-major kernel (sparse graphs): one wave per column
-  int32_t* bwd_colptr = nullptr; // [num_cols + 1] offsets of the column-sorted records
+  uint32_t* bwd_sel = nullptr;   // plan-owned workspace: [S][num_cols][L] selector words + slabs
   // two-pass backward (low row reuse): a row pass writes each edge's k products val *
   // grad_out[r, sel(c)] into the edge's slot of bwd_tbuf (CSR order), a column pass sums the
   // slots of each column's in-edges (bwd_perm, bwd_colptr)
   int32_t bwd_twopass = 0;
   int32_t bwd_tp_rows = 1;       // R: destination rows per wavefront of the row pass
-  int32_t bwd_tp_csc = 0;        // two-pass: products stored in column order; bwd_perm then
-                                 // holds the inverse map (CSR edge -> column-order slot)
-  uint32_t* bwd_erec = nullptr;  // [num_edges][2] CSR order: {column, val}
-  float* bwd_tbuf = nullptr;     // [max chunk edges][k] workspace
+  uint32_t* bwd_erec = nullptr;  // [num_edges][2] CSR order: {column | (row % R) << 26, val}
+  float* bwd_tbuf = nullptr;     // [max chunk edges][k] plan-owned workspace
+  int32_t* bwd_colptr = nullptr; // [num_cols + 1] offsets of the column-sorted edges
   // row chunks of the two-pass backward (workspace bounded by kBwdTwoPassWorkspaceCap):
   // chunk p covers destination rows [tp_rows[p], tp_rows[p+1]) = CSR edges [tp_edges[p],
   // tp_edges[p+1]); bwd_colptr2[p * NC + c] = first column-sorted position of column c whose
@@ -244,29 +211,25 @@ struct maxk_plan {
   std::vector<int32_t> tp_rows;
   std::vector<int64_t> tp_edges;
   int32_t* bwd_colptr2 = nullptr;
-  // column order of the packed backward (maxk_plan_options.col_order): bwd_corder[p] = the
-  // source column placed at position p of the column blocks (nullptr: identity). Blocks are
-  // contiguous position ranges, so the order decides which columns share an LDS block.
-  int32_t col_order = 0;
+  // column order of the column blocks (maxk_plan_options.col_order): bwd_corder[p] = the
+  // source column placed at position p of the blocks (nullptr: identity)
+  int32_t col_order = 1;
   int32_t* bwd_corder = nullptr;
-  // slab flush of shared blocks (bwd_flush 2): piece 0 of a block stores into grad_sp,
-  // piece p > 0 into its [C][k] slab region (bwd_slab_floats f32 in all, at byte
-  // bwd_slab_off of the backward workspace, behind the selector words); bwd_combine_kernel
-  // adds each block's regions in piece order. bwd_combine: one int4 {slab offset, regions,
-  // col0, ncols} per block with more than one piece
+  // slab flush of split blocks: piece 0 of a block stores into grad_sp, piece p > 0 into its
+  // [C][k] slab region (bwd_slab_floats f32 in all, at byte bwd_slab_off of the backward
+  // workspace, behind the selector words); bwd_combine_kernel adds each block's regions in
+  // piece order. bwd_combine: one int4 {slab offset, regions, col0, ncols} per block with
+  // more than one piece. bwd_slab_floats == 0 with split blocks: global float atomics
   int64_t bwd_slab_floats = 0;
   int64_t bwd_slab_off = 0;
   int4* bwd_combine = nullptr;
   int32_t n_bwd_combine = 0;
   int64_t device_bytes = 0;
-  // per-call scratch: the forward's packed CBSR records (fwd_rec) and the backward's
-  // selector words + flush slabs (bwd_sel is the base of both) or two-pass product
-  // workspace (bwd_tbuf). external_ws: the
-  // plan allocates none of them and the *_ws entry points take the caller's buffer (the
-  // Python layer passes one from torch's caching allocator on the launch stream)
+  // per-call scratch: the forward's packed CBSR records and statistics words, the backward's
+  // selector words + flush slabs or two-pass product workspace. external_ws: the plan
+  // allocates none of them and the *_ws entry points take the caller's buffer
   int32_t external_ws = 0;
   int64_t fwd_ws_bytes = 0;
   int64_t bwd_ws_bytes = 0;
-  int32_t bwd_chunk_mode = 2;    // chunk bounds in use: 1 shared rows, 2 equal edges, 3 cost
   int32_t bwd_row_order = 1;     // rows in the block streams: 1 ascending, 2 scattered
 };

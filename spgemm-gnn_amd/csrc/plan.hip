@@ -12,10 +12,11 @@
 //             are sorted by column (8-B words {column | row-in-task, val}) with window
 //             offsets for the clock-rotated sweep.
 //   backward: a stable radix sort of the edges by source-column block
-//             (hipcub::DeviceRadixSort, keys = idx / block_cols) gives the block-major,
-//             row-sorted edge list, packed as 12-B records {row * D * 4, column in block,
-//             val}; each block's range is cut into row-chunk tasks (same row bounds in every
-//             block, XCD-aware order).
+//             (hipcub::DeviceRadixSort, keys = block of the column's position) gives the
+//             block-major, row-sorted edge list, packed as 12-B records {row * D * 4, column
+//             in block, val}; each block's stream is cut into equal-edge chunk tasks emitted
+//             in order of their first row (XCD-aware). Low-reuse graphs get the two-pass
+//             metadata instead (CSR-order edge records, column pointers).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -27,8 +28,6 @@
 #include "common.h"
 
 namespace maxk {
-
-size_t acc_bytes(int acc);
 
 
 __global__ void expand_rows_kernel(const int32_t* __restrict__ ptr, int N,
@@ -167,13 +166,6 @@ static hipError_t fwd_fix_stats(const maxk_plan* p, const int32_t* ptr, const fl
   return e != hipSuccess ? e : f;
 }
 
-__global__ void invert_perm_kernel(const int32_t* __restrict__ perm, int64_t E,
-                                   int32_t* __restrict__ inv) {
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < E;
-       j += (int64_t)gridDim.x * blockDim.x)
-    inv[perm[j]] = (int32_t)j;
-}
-
 // Sort key of each edge for the backward: its source-column block c / C (a stable radix
 // sort then yields the block-major, destination-row-sorted edge list). Also validates the
 // column ids: any idx outside [0, NC) sets *bad (the compute kernels index the CBSR tables
@@ -241,18 +233,35 @@ __global__ void key_block_kernel(const uint64_t* __restrict__ k64, int64_t E, in
     blk[e] = (uint32_t)(k64[e] >> rbits);
 }
 
+// Column of each reordered edge's block position and its destination row (plan-time
+// temporaries for the records and the chunk bounds).
 __global__ void gather_bwd_kernel(const int32_t* __restrict__ perm,
                                   const int32_t* __restrict__ row_of,
-                                  const int32_t* __restrict__ idx,
-                                  const float* __restrict__ val, int64_t E,
+                                  const int32_t* __restrict__ idx, int64_t E,
                                   int32_t* __restrict__ brow, int32_t* __restrict__ bcol,
-                                  float* __restrict__ bval, const int32_t* __restrict__ colpos) {
+                                  const int32_t* __restrict__ colpos) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < E;
        j += (int64_t)gridDim.x * blockDim.x) {
     const int32_t e = perm[j];
-    if (brow) brow[j] = row_of[e];
-    if (bcol) bcol[j] = colpos ? colpos[idx[e]] : idx[e];  // the column's block position
-    bval[j] = val ? val[e] : 1.0f;
+    brow[j] = row_of[e];
+    bcol[j] = colpos ? colpos[idx[e]] : idx[e];  // the column's block position
+  }
+}
+
+// Backward records {row * D * 4 (byte offset of the grad_out row; big: the row index),
+// column within the block, val}; with row == nullptr only the val field is refreshed from
+// the CSR order through perm.
+__global__ void build_bwd_rec_kernel(const int32_t* __restrict__ perm,
+                                     const int32_t* __restrict__ row,
+                                     const int32_t* __restrict__ col,
+                                     const float* __restrict__ val, int64_t E, int C, int D,
+                                     int big, uint32_t* __restrict__ rec) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x) {  // grid_for caps the grid
+    rec[3 * e + 2] = __float_as_uint(val ? val[perm[e]] : 1.0f);
+    if (!row) continue;
+    rec[3 * e] = big ? (uint32_t)row[e] : (uint32_t)row[e] * (uint32_t)D * 4u;
+    rec[3 * e + 1] = (uint32_t)(col[e] % C);
   }
 }
 
@@ -269,43 +278,6 @@ __global__ void key_offsets_kernel(const uint32_t* __restrict__ skeys, int64_t E
   offs[b] = (int32_t)lo;
 }
 
-// Backward chunk boundaries: for block b (edges [boffs[b], boffs[b+1]) sorted by row) and row
-// bound j, the first edge of the block whose row is >= rows[j].
-__global__ void chunk_offsets_kernel(const int32_t* __restrict__ erow,
-                                     const int32_t* __restrict__ boffs, int nblocks,
-                                     const int32_t* __restrict__ rows, int nb,
-                                     int32_t* __restrict__ out) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nblocks * nb) return;
-  const int b = t / nb, j = t - b * nb;
-  int64_t lo = boffs[b], hi = boffs[b + 1];
-  const int32_t r = rows[j];
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (erow[mid] < r) lo = mid + 1; else hi = mid;
-  }
-  out[t] = (int32_t)lo;
-}
-
-// Packed backward records {row * D * 4 (byte offset of the grad_out row), column within the
-// block, val}; with perm != nullptr only the val field is refreshed from the CSR order.
-__global__ void build_bwd_rec_kernel(const int32_t* __restrict__ perm,
-                                     const int32_t* __restrict__ row,
-                                     const int32_t* __restrict__ col,
-                                     const float* __restrict__ val, int64_t E, int C, int D,
-                                     uint32_t* __restrict__ rec) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
-       e += (int64_t)gridDim.x * blockDim.x) {  // grid_for caps the grid
-    if (perm) {
-      rec[3 * e + 2] = __float_as_uint(val[perm[e]]);
-      continue;
-    }
-    rec[3 * e] = (uint32_t)row[e] * (uint32_t)D * 4u;
-    rec[3 * e + 1] = (uint32_t)(col[e] % C);
-    rec[3 * e + 2] = __float_as_uint(val[e]);
-  }
-}
-
 // Two-pass backward edge records in CSR order: {column | (row % R) << kFwdColBits, val}
 // (idx == nullptr: only the val field is refreshed).
 __global__ void build_erec_kernel(const int32_t* __restrict__ idx,
@@ -319,48 +291,10 @@ __global__ void build_erec_kernel(const int32_t* __restrict__ idx,
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Cost-balanced backward chunks (bwd_chunk_bounds 3). An edge costs 4 quarter-units; the first
-// edge of every (column block, destination row) run costs rc4 more: the block's gathers fetch
-// that row's grad_out lines once per pair, so a task's time follows its edges plus its pairs
-// (a row with 110 edges into a block - an ID-ordered community - costs about as much as 4
-// rows with one edge each). cost[e] is written in place and prefix-summed (hipcub).
-__global__ void bwd_cost_kernel(const uint32_t* __restrict__ bkey, const int32_t* __restrict__ row,
-                                int64_t E, int rc4, int64_t* __restrict__ cost) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const bool first = e == 0 || bkey[e] != bkey[e - 1] || row[e] != row[e - 1];
-    cost[e] = 4 + (first ? rc4 : 0);
-  }
-}
-
 __global__ void gather_i32_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ at,
                                   int n, int32_t* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = src[at[i]];
-}
-
-// out[i] = first e in [lo[i], hi[i]) with cum[e] > target[i] (hi[i] if none); cum ascends.
-__global__ void upper_bound_kernel(const int64_t* __restrict__ cum, const int64_t* __restrict__ target,
-                                   const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
-                                   int n, int32_t* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int64_t a = lo[i], b = hi[i];
-  const int64_t t = target[i];
-  while (a < b) {
-    const int64_t m = (a + b) >> 1;
-    if (cum[m] > t) b = m; else a = m + 1;
-  }
-  out[i] = (int32_t)a;
-}
-
-// cum[offs[b] - 1] (0 for offs[b] == 0): the cost of all blocks before b.
-__global__ void block_cost_kernel(const int64_t* __restrict__ cum, const int32_t* __restrict__ offs,
-                                  int nb, int64_t* __restrict__ out) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > nb) return;
-  out[b] = offs[b] > 0 ? cum[offs[b] - 1] : 0;
 }
 
 // Two-pass row chunks: out[p * NC + c] = first column-sorted position of column c whose row
@@ -382,11 +316,13 @@ __global__ void tp_colptr_kernel(const int32_t* __restrict__ colptr, const int32
 }
 
 // ---------------------------------------------------------------------------------------
-// Column orders of the backward blocks (maxk_plan_options.col_order).
+// Column orders of the column blocks (maxk_plan_options.col_order).
 //
 // Scattered (2): p -> column (a p + b) mod NC with gcd(a, NC) = 1, a ~ 0.618 NC: every
 // contiguous range of positions (a block) takes columns spread evenly over the ID range, so a
 // community of consecutive IDs is shared by all blocks instead of filling a few of its own.
+// The caller's order (4) is range- and permutation-checked on the host before any device
+// scatter uses it.
 __global__ void affine_order_kernel(int NC, int64_t a, int64_t b, int32_t* __restrict__ order) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= NC) return;
@@ -396,106 +332,12 @@ __global__ void affine_order_kernel(int NC, int64_t a, int64_t b, int32_t* __res
 __global__ void invert_order_kernel(const int32_t* __restrict__ order, int NC,
                                     int32_t* __restrict__ pos) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < NC) pos[order[p]] = p;
+  if (p < NC) pos[order[p]] = p;  // order is a checked permutation of [0, NC)
 }
 
-// Clustered (3): a spectral embedding of the columns by subspace iteration on M^T M, M the
-// row-normalised adjacency: X <- centre(normalise(M^T (M X))), kEmbedDims random +-1 starting
-// vectors, kEmbedIters rounds. After a few rounds X lies in the span of the leading
-// eigenvectors, where columns that appear in the same rows (a community) sit close together;
-// a Morton sort of the quantised coordinates then puts them at neighbouring positions, i.e.
-// in the same blocks. On graphs without such structure the order is as good as random.
-constexpr int kEmbedDims = 8;
-constexpr int kEmbedIters = 3;
-
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-  return x;
-}
-
-__global__ void embed_init_kernel(int NC, float* __restrict__ X) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)NC * kEmbedDims) return;
-  X[i] = (mix32((uint32_t)i * 2654435761u + 97u) & 1u) ? 1.f : -1.f;
-}
-
-// out[r] = mean over the edges (r, c) of in[c] (one wavefront per row; lanes stride over the
-// row's edges, each holding kEmbedDims partial sums, then a shuffle reduction).
-__global__ __launch_bounds__(256) void embed_spmm_kernel(const int32_t* __restrict__ ptr,
-                                                         const int32_t* __restrict__ nbr, int N,
-                                                         const float* __restrict__ in,
-                                                         float* __restrict__ out) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int r = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
-  if (r >= N) return;
-  const int e0 = ptr[r], e1 = ptr[r + 1];
-  float a[kEmbedDims];
-#pragma unroll
-  for (int j = 0; j < kEmbedDims; ++j) a[j] = 0.f;
-  for (int e = e0 + lane; e < e1; e += kWave) {
-    const float4* x = reinterpret_cast<const float4*>(in + (size_t)nbr[e] * kEmbedDims);
-    const float4 u = x[0], v = x[1];
-    a[0] += u.x; a[1] += u.y; a[2] += u.z; a[3] += u.w;
-    a[4] += v.x; a[5] += v.y; a[6] += v.z; a[7] += v.w;
-  }
-#pragma unroll
-  for (int j = 0; j < kEmbedDims; ++j)
-    for (int o = kWave / 2; o > 0; o >>= 1) a[j] += __shfl_xor(a[j], o);
-  if (lane < kEmbedDims) {
-    float s = a[0];
-#pragma unroll
-    for (int j = 1; j < kEmbedDims; ++j) s = lane == j ? a[j] : s;
-    out[(size_t)r * kEmbedDims + lane] = e1 > e0 ? s / (float)(e1 - e0) : 0.f;
-  }
-}
-
-// Per-dimension sums and sums of squares (atomics per work-group) for centring/normalising.
-__global__ __launch_bounds__(256) void embed_moments_kernel(const float* __restrict__ X, int NC,
-                                                            float* __restrict__ mom) {
-  __shared__ float sh[2 * kEmbedDims];
-  if (threadIdx.x < 2 * kEmbedDims) sh[threadIdx.x] = 0.f;
-  __syncthreads();
-  const int j = threadIdx.x & (kEmbedDims - 1);
-  float s = 0.f, q = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)NC * kEmbedDims;
-       i += (int64_t)gridDim.x * blockDim.x) {  // blockDim % kEmbedDims == 0: i % 8 == j
-    const float x = X[i];
-    s += x;
-    q += x * x;
-  }
-  atomicAdd(&sh[j], s);
-  atomicAdd(&sh[kEmbedDims + j], q);
-  __syncthreads();
-  if (threadIdx.x < 2 * kEmbedDims) atomicAdd(&mom[threadIdx.x], sh[threadIdx.x]);
-}
-
-__global__ void embed_normalise_kernel(float* __restrict__ X, int NC, const float* __restrict__ mom) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)NC * kEmbedDims) return;
-  const int j = (int)(i & (kEmbedDims - 1));
-  const float mu = mom[j] / NC;
-  const float var = fmaxf(mom[kEmbedDims + j] / NC - mu * mu, 0.f);
-  X[i] = (X[i] - mu) * (var > 0.f ? rsqrtf(var) : 0.f);
-}
-
-// 64-bit Morton key of the 8 coordinates quantised to 8 bits (+-4 standard deviations).
-__global__ void embed_morton_kernel(const float* __restrict__ X, int NC, uint64_t* __restrict__ key,
-                                    int32_t* __restrict__ ids) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= NC) return;
-  uint64_t k = 0;
-  uint32_t q[kEmbedDims];
-#pragma unroll
-  for (int j = 0; j < kEmbedDims; ++j) {
-    const float v = X[(size_t)c * kEmbedDims + j] * 32.f + 128.f;
-    q[j] = (uint32_t)fminf(fmaxf(v, 0.f), 255.f);
-  }
-#pragma unroll
-  for (int b = 7; b >= 0; --b)
-#pragma unroll
-    for (int j = 0; j < kEmbedDims; ++j) k = (k << 1) | ((q[j] >> b) & 1u);
-  key[c] = k;
-  ids[c] = c;
+__global__ void iota_kernel(int n, int32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = i;
 }
 
 static void dfree(void* q) { if (q) (void)hipFree(q); }
@@ -517,9 +359,6 @@ static void free_plan(maxk_plan* p) {
   dfree(p->zero_rows);
   dfree(p->bwd_tasks);
   dfree(p->bwd_perm);
-  dfree(p->bwd_row);
-  dfree(p->bwd_col);
-  dfree(p->bwd_val);
   dfree(p->bwd_rec);
   dfree(p->bwd_sel);
   dfree(p->bwd_colptr);
@@ -531,87 +370,35 @@ static void free_plan(maxk_plan* p) {
   delete p;
 }
 
-// Column order of the backward blocks (col_order 2 scattered, 3 clustered, 4 the caller's):
-// *order = device int32 [NC], order[p] = column at position p. row_of: row of each CSR edge.
-static hipError_t build_col_order(int mode, const int32_t* ptr, const int32_t* idx,
-                                  const int32_t* row_of, int N, int NC, int64_t E,
-                                  const int32_t* user, hipStream_t s, int32_t** order) {
+// Column order of the column blocks (col_order 2 scattered, 4 the caller's): *order = device
+// int32 [NC], order[p] = column at position p. The caller's order must be a permutation of
+// [0, NC): *bad is set otherwise, and nothing is scattered with it.
+static hipError_t build_col_order(int mode, int NC, const int32_t* user, hipStream_t s,
+                                  int32_t** order, bool* bad) {
+  *bad = false;
   hipError_t e = hipMalloc(order, sizeof(int32_t) * (size_t)NC);
   if (e != hipSuccess) return e;
-  const int g = (NC + 255) / 256;
-  if (mode == 4) return hipMemcpyAsync(*order, user, sizeof(int32_t) * (size_t)NC,
-                                       hipMemcpyDeviceToDevice, s);
-  if (mode == 2 || E == 0) {
-    // a ~ 0.618 NC, coprime with NC (b: a fixed offset)
-    int64_t a = std::max<int64_t>(1, (int64_t)(0.6180339887 * NC));
-    auto gcd = [](int64_t x, int64_t y) { while (y) { const int64_t t = x % y; x = y; y = t; } return x; };
-    while (gcd(a, NC) != 1) ++a;
-    hipLaunchKernelGGL(affine_order_kernel, dim3(g), dim3(256), 0, s, NC, a % NC,
-                       (int64_t)(NC / 3), *order);
-    return hipGetLastError();
+  if (mode == 4) {
+    std::vector<int32_t> ho(NC);
+    e = hipMemcpyAsync(ho.data(), user, sizeof(int32_t) * NC, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    std::vector<uint8_t> seen(NC, 0);
+    for (int i = 0; i < NC && !*bad; ++i) {
+      const int32_t c = ho[i];
+      *bad = c < 0 || c >= NC || seen[c];
+      if (!*bad) seen[c] = 1;
+    }
+    if (*bad) return hipSuccess;
+    return hipMemcpyAsync(*order, ho.data(), sizeof(int32_t) * NC, hipMemcpyHostToDevice, s);
   }
-  // clustered: column CSR (rows sorted by column), subspace iteration, Morton sort
-  uint32_t *kin = nullptr, *kout = nullptr;
-  int32_t *crow = nullptr, *cptr = nullptr, *ids = nullptr;
-  float *X = nullptr, *Y = nullptr, *mom = nullptr;
-  uint64_t *mk = nullptr, *mk2 = nullptr;
-  void* tmp = nullptr;
-  auto cleanup = [&]() {
-    dfree(kin); dfree(kout); dfree(crow); dfree(cptr); dfree(ids); dfree(X); dfree(Y);
-    dfree(mom); dfree(mk); dfree(mk2); dfree(tmp);
-  };
-#define ORD_TRY(x)                      \
-  do {                                  \
-    const hipError_t e_ = (x);          \
-    if (e_ != hipSuccess) {             \
-      cleanup();                        \
-      return e_;                        \
-    }                                   \
-  } while (0)
-  int cbits = 1;
-  while ((1ll << cbits) < (long long)NC) ++cbits;
-  ORD_TRY(hipMalloc(&kin, sizeof(uint32_t) * E));
-  ORD_TRY(hipMalloc(&kout, sizeof(uint32_t) * E));
-  ORD_TRY(hipMalloc(&crow, sizeof(int32_t) * E));
-  ORD_TRY(hipMemcpyAsync(kin, idx, sizeof(int32_t) * E, hipMemcpyDeviceToDevice, s));
-  size_t tb = 0;
-  ORD_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, row_of, crow, (int)E, 0, cbits, s));
-  ORD_TRY(hipMalloc(&tmp, std::max<size_t>(tb, 16)));
-  ORD_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, row_of, crow, (int)E, 0, cbits, s));
-  ORD_TRY(hipMalloc(&cptr, sizeof(int32_t) * ((size_t)NC + 1)));
-  hipLaunchKernelGGL(key_offsets_kernel, dim3(NC / 256 + 1), dim3(256), 0, s, kout, E, NC, cptr);
-  ORD_TRY(hipGetLastError());
-  dfree(kin); kin = nullptr;
-  ORD_TRY(hipMalloc(&X, sizeof(float) * kEmbedDims * (size_t)NC));
-  ORD_TRY(hipMalloc(&Y, sizeof(float) * kEmbedDims * (size_t)std::max(N, 1)));
-  ORD_TRY(hipMalloc(&mom, sizeof(float) * 2 * kEmbedDims));
-  const int gx = (int)(((int64_t)NC * kEmbedDims + 255) / 256);
-  hipLaunchKernelGGL(embed_init_kernel, dim3(gx), dim3(256), 0, s, NC, X);
-  for (int it = 0; it < kEmbedIters; ++it) {
-    hipLaunchKernelGGL(embed_spmm_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, idx, N, X, Y);
-    hipLaunchKernelGGL(embed_spmm_kernel, dim3((NC + 3) / 4), dim3(256), 0, s, cptr, crow, NC, Y, X);
-    ORD_TRY(hipMemsetAsync(mom, 0, sizeof(float) * 2 * kEmbedDims, s));
-    hipLaunchKernelGGL(embed_moments_kernel, dim3(std::min(gx, 1024)), dim3(256), 0, s, X, NC, mom);
-    hipLaunchKernelGGL(embed_normalise_kernel, dim3(gx), dim3(256), 0, s, X, NC, mom);
-    ORD_TRY(hipGetLastError());
-  }
-  ORD_TRY(hipMalloc(&mk, sizeof(uint64_t) * NC));
-  ORD_TRY(hipMalloc(&mk2, sizeof(uint64_t) * NC));
-  ORD_TRY(hipMalloc(&ids, sizeof(int32_t) * NC));
-  hipLaunchKernelGGL(embed_morton_kernel, dim3(g), dim3(256), 0, s, X, NC, mk, ids);
-  ORD_TRY(hipGetLastError());
-  size_t tb2 = 0;
-  ORD_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, mk, mk2, ids, *order, NC, 0, 64, s));
-  if (tb2 > tb) {
-    dfree(tmp);
-    tmp = nullptr;
-    ORD_TRY(hipMalloc(&tmp, tb2));
-  }
-  ORD_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb2, mk, mk2, ids, *order, NC, 0, 64, s));
-  ORD_TRY(hipStreamSynchronize(s));
-  cleanup();
-#undef ORD_TRY
-  return hipSuccess;
+  // a ~ 0.618 NC, coprime with NC (b: a fixed offset)
+  int64_t a = std::max<int64_t>(1, (int64_t)(0.6180339887 * NC));
+  auto gcd = [](int64_t x, int64_t y) { while (y) { const int64_t t = x % y; x = y; y = t; } return x; };
+  while (gcd(a, NC) != 1) ++a;
+  hipLaunchKernelGGL(affine_order_kernel, dim3((NC + 255) / 256), dim3(256), 0, s, NC, a % NC,
+                     (int64_t)(NC / 3), *order);
+  return hipGetLastError();
 }
 
 // Forward task list from a host copy of ptr.
@@ -679,7 +466,8 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                                    int32_t N, int32_t NC, int64_t E, int32_t D, int32_t k,
                                    const maxk_plan_options* opts, void* stream,
                                    maxk_plan** out_plan) {
-  // the version-1 layout: a binding of ABI 1 passes a struct of exactly these bytes
+  // the last layout shipped under ABI 1 (through bwd_tp_store, 144 bytes); a binding of the
+  // round-1 120-byte layout passes its size to maxk_plan_create_sized
   return maxk_plan_create_sized(ptr, idx, val, N, NC, E, D, k, opts,
                                 opts ? MAXK_PLAN_OPTIONS_V1_BYTES : 0, nullptr, stream, out_plan);
 }
@@ -706,34 +494,103 @@ extern "C" int maxk_plan_create_sized(const int32_t* ptr, const int32_t* idx, co
   return plan_create_impl(ptr, idx, val, N, NC, E, D, k, o, col_order, stream, out_plan);
 }
 
+// Options whose other values selected kernel organisations that ABI 3 removed (slower on every
+// measured configuration and never chosen automatically): only 0 and the
+// behaviour that remains are accepted.
+#define MAXK_CHECK_REMOVED(cond, msg)                                                      \
+  do {                                                                                     \
+    if (!(cond)) {                                                                         \
+      ::maxk::set_error(std::string("maxk_plan_create: ") + msg + " (removed in ABI 3)");  \
+      return MAXK_ERR_UNSUPPORTED;                                                         \
+    }                                                                                      \
+  } while (0)
+
+static int check_options(const maxk_plan_options& o) {
+  MAXK_CHECK_ARG(o.fwd_tile_rows >= 0 && o.fwd_tile_rows <= kFwdMaxTileRows,
+                 "maxk_plan_create: fwd_tile_rows must be in [0, 64]");
+  MAXK_CHECK_ARG(o.fwd_accumulator >= 0 && o.fwd_accumulator <= MAXK_ACC_F32_CAS &&
+                     o.bwd_accumulator >= 0 && o.bwd_accumulator <= MAXK_ACC_F32_CAS,
+                 "maxk_plan_create: unknown accumulator kind");
+  MAXK_CHECK_REMOVED(o.fwd_accumulator != MAXK_ACC_F32_CAS, "fwd_accumulator = f32 CAS");
+  MAXK_CHECK_REMOVED(o.bwd_accumulator != MAXK_ACC_F64, "bwd_accumulator = f64");
+  MAXK_CHECK_ARG(o.bwd_lds_bytes >= 0 && o.bwd_lds_bytes <= kBwdLdsBudget && o.bwd_tasks_per_cu >= 0 &&
+                     o.fwd_task_cap >= 0 && o.bwd_min_task_edges >= 0 && o.bwd_piece_edges >= 0 &&
+                     o.bwd_tp_chunks >= 0 && o.fwd_rot_windows >= 0 && o.fwd_rot_rate >= 0,
+                 "maxk_plan_create: bad option value (negative, or bwd_lds_bytes > 160 KiB)");
+  MAXK_CHECK_ARG(o.bwd_features_per_lane >= 0 && o.bwd_features_per_lane <= 4 &&
+                     o.bwd_features_per_lane != 3,
+                 "maxk_plan_create: bwd_features_per_lane must be 0, 2 or 4");
+  MAXK_CHECK_REMOVED(o.bwd_features_per_lane != 1, "bwd_features_per_lane = 1");
+  MAXK_CHECK_REMOVED(o.fwd_phases <= 1, "fwd_phases > 1");
+  MAXK_CHECK_REMOVED(o.fwd_persistent == 0, "fwd_persistent");
+  MAXK_CHECK_REMOVED(o.fwd_unroll == 0 || o.fwd_unroll == 8, "fwd_unroll other than 8");
+  MAXK_CHECK_ARG(o.bwd_unroll == 0 || o.bwd_unroll == 8 || o.bwd_unroll == 12 ||
+                     o.bwd_unroll == 16,
+                 "maxk_plan_create: bwd_unroll must be 0, 8, 12 or 16");
+  MAXK_CHECK_REMOVED(o.bwd_order == 0, "bwd_order = 1 (heavy-first tasks)");
+  MAXK_CHECK_ARG(o.bwd_slot_groups >= 0 && o.bwd_slot_groups <= 64 &&
+                     (o.bwd_slot_groups & (o.bwd_slot_groups - 1)) == 0,
+                 "maxk_plan_create: bwd_slot_groups must be 0 or a power of two <= 64");
+  MAXK_CHECK_REMOVED(o.bwd_acc_pad == 0 || o.bwd_acc_pad == 2, "bwd_acc_pad = 1");
+  MAXK_CHECK_REMOVED(o.bwd_sel_lds == 0 || o.bwd_sel_lds == 1, "bwd_sel_lds = 2");
+  MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 2,
+                 "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.bwd_algo >= 0 && o.bwd_algo <= 3,
+                 "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks) or 3 (two-pass)");
+  MAXK_CHECK_REMOVED(o.bwd_algo != 2, "bwd_algo = 2 (column-major)");
+  MAXK_CHECK_REMOVED(o.fwd_waves == 0 || o.fwd_waves == 4, "fwd_waves other than 4");
+  MAXK_CHECK_ARG(o.bwd_waves == 0 || o.bwd_waves == 8 || o.bwd_waves == 12,
+                 "maxk_plan_create: bwd_waves must be 0, 8 or 12");
+  MAXK_CHECK_REMOVED((o.fwd_prefetch == 0 || o.fwd_prefetch == 2) &&
+                         (o.bwd_prefetch == 0 || o.bwd_prefetch == 2),
+                     "fwd_prefetch / bwd_prefetch = 1");
+  MAXK_CHECK_REMOVED(o.fwd_record_bytes == 0, "fwd_record_bytes");
+  MAXK_CHECK_REMOVED(o.fwd_branchless == 0 || o.fwd_branchless == 1, "fwd_branchless = 2");
+  MAXK_CHECK_ARG(o.fwd_chunk3 >= 0 && o.fwd_chunk3 <= 2,
+                 "maxk_plan_create: fwd_chunk3 must be 0, 1 or 2");
+  MAXK_CHECK_REMOVED(o.bwd_cas64 == 0 || o.bwd_cas64 == 1, "bwd_cas64 = 2");
+  MAXK_CHECK_REMOVED(o.quad_loads == 0, "quad_loads");
+  MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
+                 "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.external_workspace == 0 || o.external_workspace == 1,
+                 "maxk_plan_create: external_workspace must be 0 or 1");
+  MAXK_CHECK_ARG(o.bwd_flush >= 0 && o.bwd_flush <= 2,
+                 "maxk_plan_create: bwd_flush must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.bwd_chunk_bounds >= 0 && o.bwd_chunk_bounds <= 3,
+                 "maxk_plan_create: bwd_chunk_bounds must be 0 or 2");
+  MAXK_CHECK_REMOVED(o.bwd_chunk_bounds == 0 || o.bwd_chunk_bounds == 2,
+                     "bwd_chunk_bounds 1 (shared rows) / 3 (equal cost)");
+  MAXK_CHECK_ARG(o.fwd_fixed >= 0 && o.fwd_fixed <= 2,
+                 "maxk_plan_create: fwd_fixed must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.bwd_tp_store >= 0 && o.bwd_tp_store <= 2,
+                 "maxk_plan_create: bwd_tp_store must be 0 or 1");
+  MAXK_CHECK_REMOVED(o.bwd_tp_store != 2, "bwd_tp_store = 2 (column-order products)");
+  MAXK_CHECK_REMOVED(o.bwd_row_cost == 0, "bwd_row_cost");
+  MAXK_CHECK_ARG(o.col_order >= 0 && o.col_order <= 4,
+                 "maxk_plan_create: col_order must be 0, 1, 2 or 4");
+  MAXK_CHECK_REMOVED(o.col_order != 3, "col_order = 3 (clustered)");
+  MAXK_CHECK_ARG(o.bwd_row_order >= 0 && o.bwd_row_order <= 2,
+                 "maxk_plan_create: bwd_row_order must be 0, 1 or 2");
+  return MAXK_OK;
+}
+
+static int device_cus() {
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+      prop.multiProcessorCount > 0)
+    return prop.multiProcessorCount;
+  return 256;
+}
+
 static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float* val, int32_t N,
                             int32_t NC, int64_t E, int32_t D, int32_t k,
                             const maxk_plan_options& o, const int32_t* user_order, void* stream,
                             maxk_plan** out_plan) {
-  MAXK_CHECK_ARG(o.fwd_tile_rows >= 0 && o.fwd_tile_rows <= kFwdMaxTileRows,
-                 "maxk_plan_create: fwd_tile_rows must be in [0, 32]");
-  MAXK_CHECK_ARG(o.fwd_accumulator >= 0 && o.fwd_accumulator <= MAXK_ACC_F32_CAS &&
-                     o.bwd_accumulator >= 0 && o.bwd_accumulator <= MAXK_ACC_F32_CAS,
-                 "maxk_plan_create: unknown accumulator kind");
-  MAXK_CHECK_ARG(o.fwd_fixed >= 0 && o.fwd_fixed <= 2,
-                 "maxk_plan_create: fwd_fixed must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_row_cost >= 0 && o.bwd_row_cost <= 4096,
-                 "maxk_plan_create: bwd_row_cost must be in [0, 4096]");
-  MAXK_CHECK_ARG(o.col_order >= 0 && o.col_order <= 4,
-                 "maxk_plan_create: col_order must be 0 .. 4");
+  *out_plan = nullptr;
+  if (const int rc = check_options(o)) return rc;
   MAXK_CHECK_ARG(o.col_order != 4 || user_order != nullptr || NC == 0,
                  "maxk_plan_create: col_order 4 needs the col_order argument");
-  MAXK_CHECK_ARG(o.bwd_tp_chunks >= 0, "maxk_plan_create: bwd_tp_chunks must be >= 0");
-  MAXK_CHECK_ARG(o.bwd_row_order >= 0 && o.bwd_row_order <= 2,
-                 "maxk_plan_create: bwd_row_order must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_tp_store >= 0 && o.bwd_tp_store <= 2,
-                 "maxk_plan_create: bwd_tp_store must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_lds_bytes >= 0 && o.bwd_lds_bytes <= 160 * 1024 &&
-                     o.bwd_tasks_per_cu >= 0 && o.fwd_task_cap >= 0 && o.fwd_phases >= 0 &&
-                     o.bwd_min_task_edges >= 0 &&
-                     o.fwd_phases <= 64,
-                 "maxk_plan_create: bad option value");
-  *out_plan = nullptr;
   MAXK_CHECK_ARG(NC >= 0 && (E == 0 || NC > 0), "maxk_plan_create: num_cols out of range");
   if ((uint32_t)NC > kFwdColMask + 1u) {
     set_error("maxk_plan_create: more than 2^26 source columns is not supported");
@@ -746,53 +603,6 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   MAXK_CHECK_ARG(ptr != nullptr && (E == 0 || idx != nullptr), "maxk_plan_create: null pointer");
   hipStream_t s = (hipStream_t)stream;
 
-  MAXK_CHECK_ARG((o.fwd_unroll == 0 || o.fwd_unroll == 8 || o.fwd_unroll == 16) &&
-                     (o.bwd_unroll == 0 || o.bwd_unroll == 4 || o.bwd_unroll == 8 ||
-                      o.bwd_unroll == 12 || o.bwd_unroll == 16),
-                 "maxk_plan_create: unroll must be 0, 8 or 16 (backward also 4 or 12)");
-  MAXK_CHECK_ARG(o.bwd_algo >= 0 && o.bwd_algo <= 3,
-                 "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks), 2 (CSC) or 3 "
-                 "(two-pass)");
-  MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 2,
-                 "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_sel_lds >= 0 && o.bwd_sel_lds <= 2,
-                 "maxk_plan_create: bwd_sel_lds must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.quad_loads >= 0 && o.quad_loads <= 2,
-                 "maxk_plan_create: quad_loads must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_cas64 >= 0 && o.bwd_cas64 <= 2,
-                 "maxk_plan_create: bwd_cas64 must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_acc_pad >= 0 && o.bwd_acc_pad <= 2,
-                 "maxk_plan_create: bwd_acc_pad must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_order == 0 || o.bwd_order == 1,
-                 "maxk_plan_create: bwd_order must be 0 or 1");
-  MAXK_CHECK_ARG(o.bwd_slot_groups >= 0 && o.bwd_slot_groups <= 64 &&
-                     (o.bwd_slot_groups & (o.bwd_slot_groups - 1)) == 0,
-                 "maxk_plan_create: bwd_slot_groups must be 0 or a power of two <= 64");
-  MAXK_CHECK_ARG((o.fwd_waves == 0 || o.fwd_waves == 4 || o.fwd_waves == 6 || o.fwd_waves == 8) &&
-                     (o.bwd_waves == 0 || o.bwd_waves == 8 || o.bwd_waves == 12 ||
-                      o.bwd_waves == 16),
-                 "maxk_plan_create: fwd_waves must be 0, 4, 6 or 8 and bwd_waves 0, 8, 12 or 16");
-  MAXK_CHECK_ARG(o.fwd_prefetch >= 0 && o.fwd_prefetch <= 2 && o.bwd_prefetch >= 0 &&
-                     o.bwd_prefetch <= 2 && o.fwd_branchless >= 0 && o.fwd_branchless <= 2,
-                 "maxk_plan_create: fwd_prefetch / bwd_prefetch / fwd_branchless must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.fwd_record_bytes == 0 ||
-                     (o.fwd_record_bytes % 16 == 0 &&
-                      (o.fwd_chunk3 == 1 || (o.fwd_record_bytes >= 5 * k && k % 4 == 0))),
-                 "maxk_plan_create: fwd_record_bytes must be 0 or a multiple of 16 >= 5k");
-  MAXK_CHECK_ARG(o.fwd_chunk3 >= 0 && o.fwd_chunk3 <= 2, "maxk_plan_create: fwd_chunk3 must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_features_per_lane == 0 || o.bwd_features_per_lane == 1 ||
-                     (o.bwd_features_per_lane == 2 && k % 2 == 0) ||
-                     (o.bwd_features_per_lane == 4 && k % 4 == 0),
-                 "maxk_plan_create: bwd_features_per_lane must be 0, 1, 2 (k % 2 == 0) or 4 (k % 4 == 0)");
-  MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
-                 "maxk_plan_create: fwd_two_tables must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.external_workspace == 0 || o.external_workspace == 1,
-                 "maxk_plan_create: external_workspace must be 0 or 1");
-  MAXK_CHECK_ARG(o.bwd_flush >= 0 && o.bwd_flush <= 2,
-                 "maxk_plan_create: bwd_flush must be 0, 1 or 2");
-  MAXK_CHECK_ARG(o.bwd_piece_edges >= 0, "maxk_plan_create: bwd_piece_edges must be >= 0");
-  MAXK_CHECK_ARG(o.bwd_chunk_bounds >= 0 && o.bwd_chunk_bounds <= 3,
-                 "maxk_plan_create: bwd_chunk_bounds must be 0, 1, 2 or 3");
   maxk_plan* p = new maxk_plan();
   p->external_ws = o.external_workspace;
   p->num_nodes = N;
@@ -802,74 +612,82 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   p->dim_k = k;
   p->src_ptr = ptr;
   p->src_idx = idx;
+  p->cus = device_cus();
+  const int cus = p->cus;
   p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
-  p->fwd_unroll = o.fwd_unroll ? o.fwd_unroll : kFwdUnroll;
-  p->bwd_unroll = o.bwd_unroll ? o.bwd_unroll : kBwdUnroll;
-  // defaults measured on the Reddit-shaped graph (tools/sweep.py, profiles/r01)
-  p->fwd_waves = o.fwd_waves ? o.fwd_waves : kFwdWaves;
-  p->bwd_waves = o.bwd_waves ? o.bwd_waves : (k >= 32 ? 12 : kBwdWaves);
-  p->fwd_prefetch = o.fwd_prefetch == 1;
-  p->bwd_prefetch = o.bwd_prefetch == 1;
   // lane-chunk records by default where the 4-values-per-lane layout fits k badly (Reddit:
   // k = 8 0.95 vs 1.02 ms, k = 24 1.93 vs 2.09 ms; k = 16 / 32 / 64 are slower with chunks),
-  // and for every k % 4 != 0 (the alternative is the 1-feature-per-lane kernel)
+  // and for every k % 4 != 0 up to 192 (beyond: one lane per feature, f64)
   p->fwd_chunk3 = (o.fwd_chunk3 == 1 || (o.fwd_chunk3 == 0 && k % 16 != 0)) && (k + 2) / 3 <= kWave;
-  p->fwd_branchless = o.fwd_branchless == 0 ? (k >= 16 || p->fwd_chunk3) : (o.fwd_branchless == 1);
-  {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
-        prop.multiProcessorCount > 0)
-      p->cus = prop.multiProcessorCount;
-  }
-  p->fwd_acc = o.fwd_accumulator ? o.fwd_accumulator : MAXK_ACC_F64;
-  // Fixed-point forward (LdsFix; the packed 4-values-per-lane and lane-chunk kernels with the
-  // f64 kind). Measured (tools/fwd_fixed_sweep.py, fixed vs f64 ms): Reddit k = 16 1.22 / 1.34,
+  // Fixed-point forward (LdsFix; the packed 4-values-per-lane and lane-chunk kernels).
+  // Measured (tools/fwd_fixed_sweep.py, fixed vs f64 ms): Reddit k = 16 1.22 / 1.34,
   // k = 24 1.57 / 1.95, k = 32 1.80 / 2.46, k = 64 3.45 / 4.81; ogbn-proteins k = 16 0.80 / 0.93,
   // k = 64 2.22 / 3.37. Not by default at k < 16 (Reddit k = 8 0.93 / 0.91, the stats pass
   // included) or on tables past the packed-record thresholds, whose gathers are HBM-bound
   // (ogbn-products k = 16 3.14 / 3.02, k = 32 4.86 / 4.78).
-  {
-    const bool big = (double)std::max(NC, 1) * 5.0 * k >
-                     (k >= 32 ? kFwdPackedTableBytes : kFwdPackedTableBytes16);
-    p->fwd_fixed = (o.fwd_fixed == 1 || (o.fwd_fixed == 0 && k >= 16 && !big)) &&
-                   p->fwd_acc == MAXK_ACC_F64 && (k % 4 == 0 || p->fwd_chunk3);
-  }
-  p->bwd_acc = o.bwd_accumulator ? o.bwd_accumulator : MAXK_ACC_F32_CAS;
+  const bool big_table = (double)std::max(NC, 1) * 5.0 * k >
+                         (k >= 32 ? kFwdPackedTableBytes : kFwdPackedTableBytes16);
+  p->fwd_fixed = (o.fwd_fixed == 1 || (o.fwd_fixed == 0 && k >= 16 && !big_table)) &&
+                 (k % 4 == 0 || p->fwd_chunk3);
+  // forward quad-shared edge-word loads with the fixed-point kernel (k = 16 1.19 -> 1.16 ms,
+  // k = 32 1.81 -> 1.78); neutral-to-slower on the f64 kernel
+  p->fwd_quad = p->fwd_fixed;
+
+  // ---- backward kernel shape (column blocks)
+  const int lds_budget = o.bwd_lds_bytes ? o.bwd_lds_bytes : kBwdLdsBudget;
   // k = 8: two slots per lane, so a gather instruction covers 16 edges (4 lanes per edge)
   // instead of 32, when a column block sees few edges per grad_out row (32 edges then span
   // ~4 rows: Reddit, 7.7 edges per (block, row), 1.151 -> 1.125 ms with unroll 12); with
   // more (ogbn-proteins, 15) the 32 edges share ~2 rows and 4 slots per lane stay faster
-  // (0.831 vs 0.877 ms). Edges per (block, row) estimated from the LDS budget.
+  // (0.831 vs 0.877 ms). Edges per (block, row) estimated from the LDS budget. k = 2 mod 4:
+  // two slots per lane need no padding slot.
   bool two_slots = false;
   if (k == 8 && N > 0 && NC > 0) {
-    const int lds0 = o.bwd_lds_bytes ? o.bwd_lds_bytes : kBwdLdsBudget;
-    const double c0 = std::min<double>(NC, (lds0 - 16) / (5.0 * k));
+    const double c0 = std::min<double>(NC, (lds_budget - 16) / (5.0 * k));
     two_slots = (double)E / N * c0 / NC < 10.0;
   }
-  p->bwd_feats = o.bwd_features_per_lane ? o.bwd_features_per_lane
-                                         : (two_slots ? 2 : (k % 4 == 0 ? 4 : 1));
-  if (p->bwd_feats == 2 && o.bwd_unroll == 0) p->bwd_unroll = 12;
+  int F = o.bwd_features_per_lane ? o.bwd_features_per_lane
+                                  : (two_slots || (k % 4 == 2 && k <= 2 * kWave) ? 2 : 4);
+  if (F == 2 && (k + 1) / 2 > kWave) F = 4;  // L = k / 2 lanes must fit a wave
+  p->bwd_feats = F;
+  // Slot groups: the k selector slots are split into S groups of k/S consecutive (sorted,
+  // hence clustered) slots, one work-group per (block, group). An edge then touches the few
+  // grad_out lines its group's features fall in, and a block spans S times more columns.
+  // Auto at k >= 32 with few edges per (block, row): two groups (Reddit, ~1.9 edges per
+  // block row at k = 32: 2.88 -> 2.66 ms; k = 64, ~1.0: 4.88 -> 4.71; ogbn-proteins k = 64,
+  // ~1.9: 3.32 -> 3.25); with more reuse one group stays faster (ogbn-proteins k = 32, ~3.1:
+  // 1.82 vs 1.86).
+  const int kF = (k + F - 1) / F * F;  // k padded to whole lanes
+  int S = o.bwd_slot_groups ? o.bwd_slot_groups : 1;
+  if (o.bwd_slot_groups == 0 && F == 4 && k >= 32 && k % 8 == 0 && N > 0 && NC > 0) {
+    const double c1 = std::min<double>(NC, (lds_budget - 16) / (5.0 * k));
+    if ((double)E / N * c1 / NC < 2.5) S = 2;
+  }
+  while (S > 1 && kF % (F * S) != 0) S >>= 1;
+  p->bwd_slot_groups = S;
+  p->bwd_kp = kF;
+  p->bwd_ks = kF / S;  // accumulators per column and group (64-bit CAS pairs: unpadded)
+  p->bwd_unroll = o.bwd_unroll ? o.bwd_unroll : (F == 2 ? 12 : 8);
+  p->bwd_waves = o.bwd_waves ? o.bwd_waves : (k >= 32 ? 12 : 8);
+  p->bwd_big = (uint64_t)N * (uint64_t)D * 4u > 0xffffffffull;  // 32-bit buffer offsets
+  // bytes of LDS per column: ks f32 accumulators + ks staged selector bytes
+  int C = std::max(1, (lds_budget - 16) / (5 * p->bwd_ks));
+  C = std::min(C, std::max(NC, 1));
 
   int32_t* row_of = nullptr;
   uint32_t* keys_in = nullptr;
   uint32_t* keys_out = nullptr;
   int32_t* ids_in = nullptr;
+  int32_t* brow = nullptr;   // destination row / block position of each reordered edge
+  int32_t* bcol = nullptr;
   void* temp = nullptr;
-  int64_t* d_offs = nullptr;
+  int32_t* d_offs = nullptr;
   int* d_bad = nullptr;
-  int32_t* order = nullptr;   // column order: position -> column (col_order 2..4)
+  int32_t* order = nullptr;   // column order: position -> column (col_order 2, 4)
   int32_t* colpos = nullptr;  // column -> position
   auto fail = [&](int rc) {
-    dfree(order);
-    dfree(colpos);
-    dfree(row_of);
-    dfree(keys_in);
-    dfree(keys_out);
-    dfree(ids_in);
-    dfree(temp);
-    dfree(d_offs);
-    dfree(d_bad);
+    dfree(order); dfree(colpos); dfree(row_of); dfree(keys_in); dfree(keys_out); dfree(ids_in);
+    dfree(brow); dfree(bcol); dfree(temp); dfree(d_offs); dfree(d_bad);
     free_plan(p);
     return rc;
   };
@@ -881,6 +699,13 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       return fail((int)_e);                                                       \
     }                                                                             \
   } while (0)
+  auto need_row_of = [&]() -> hipError_t {
+    if (row_of || E == 0) return hipSuccess;
+    hipError_t e = hipMalloc(&row_of, sizeof(int32_t) * E);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
+    return hipGetLastError();
+  };
 
   // ---------------- forward
   std::vector<int32_t> hp(N + 1);
@@ -896,44 +721,21 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       return fail(MAXK_ERR_INVALID_ARG);
     }
   }
-  // ---------------- column order (col_order 2 scattered, 3 clustered, 4 the caller's): the
-  // backward's packed kernels take their column blocks as position ranges of it. The forward
-  // keeps its column-sorted sweep: sweeping in the clustered order measured much slower
-  // (shuffled 41-community Reddit-size graph: k = 16 1.07 -> 1.36 ms, k = 32 1.61 -> 2.75)
+  // ---------------- column order (col_order 2 scattered, 4 the caller's): the column blocks
+  // take position ranges of it. The forward keeps its column-sorted sweep (sweeping in a
+  // clustered order measured much slower: k = 16 1.07 -> 1.36 ms, k = 32 1.61 -> 2.75)
   const int order_mode = o.col_order == 0 ? 1 : o.col_order;
   if (order_mode >= 2 && NC > 0) {
-    if (E > 0) {
-      PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
-      hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
-      PLAN_TRY(hipGetLastError());
+    bool bad_order = false;
+    PLAN_TRY(build_col_order(order_mode, NC, user_order, s, &order, &bad_order));
+    if (bad_order) {
+      set_error("maxk_plan_create: col_order is not a permutation of [0, num_cols)");
+      return fail(MAXK_ERR_INVALID_ARG);
     }
-    PLAN_TRY(build_col_order(order_mode, ptr, idx, row_of, N, NC, E, user_order, s, &order));
     PLAN_TRY(hipMalloc(&colpos, sizeof(int32_t) * NC));
-    PLAN_TRY(hipMemsetAsync(colpos, 0xff, sizeof(int32_t) * NC, s));
     hipLaunchKernelGGL(invert_order_kernel, dim3((NC + 255) / 256), dim3(256), 0, s, order, NC, colpos);
     PLAN_TRY(hipGetLastError());
-    if (order_mode == 4) {  // the caller's order must be a permutation of [0, NC)
-      std::vector<int32_t> ho(NC), hc(NC);
-      PLAN_TRY(hipMemcpyAsync(ho.data(), order, sizeof(int32_t) * NC, hipMemcpyDeviceToHost, s));
-      PLAN_TRY(hipStreamSynchronize(s));
-      bool ok = true;
-      for (int i = 0; i < NC && ok; ++i) ok = ho[i] >= 0 && ho[i] < NC;
-      if (ok) {
-        PLAN_TRY(hipMemcpyAsync(hc.data(), colpos, sizeof(int32_t) * NC, hipMemcpyDeviceToHost, s));
-        PLAN_TRY(hipStreamSynchronize(s));
-        for (int i = 0; i < NC && ok; ++i) ok = hc[i] >= 0 && ho[hc[i]] == i;
-      }
-      if (!ok) {
-        set_error("maxk_plan_create: col_order is not a permutation of [0, num_cols)");
-        return fail(MAXK_ERR_INVALID_ARG);
-      }
-    }
   }
-  auto drop_order = [&]() {
-    dfree(order);
-    dfree(colpos);
-    order = colpos = nullptr;
-  };
 
   std::vector<FwdTask> ftasks;
   std::vector<int32_t> zrows;
@@ -943,21 +745,21 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   if (!ftasks.empty()) {
     // permuted edge order (see fwd_key_kernel): tasks keep their CSR edge sets
     const int nt = (int)ftasks.size();
-    std::vector<int32_t> order(nt);
-    for (int i = 0; i < nt; ++i) order[i] = i;
+    std::vector<int32_t> torder(nt);
+    for (int i = 0; i < nt; ++i) torder[i] = i;
     // by first edge, and among equal first edges the empty tasks (an edgeless tile shares its
     // e0 with the next tile) before the one task that owns edges there: fwd_key_kernel takes
     // the LAST task whose first edge is <= e (an edgeless tile ordered last took the next
     // tile's edges, whose rows then stayed zero: tests/test_gpu_fuzz.py)
-    std::sort(order.begin(), order.end(), [&](int a, int b) {
+    std::sort(torder.begin(), torder.end(), [&](int a, int b) {
       if (ftasks[a].e0 != ftasks[b].e0) return ftasks[a].e0 < ftasks[b].e0;
       return ftasks[a].e1 < ftasks[b].e1;
     });
     std::vector<int32_t> starts(nt), ranks(nt), row0s(nt);
     for (int i = 0; i < nt; ++i) {
-      starts[i] = ftasks[order[i]].e0;
-      ranks[i] = order[i];
-      row0s[i] = ftasks[order[i]].row0;
+      starts[i] = ftasks[torder[i]].e0;
+      ranks[i] = torder[i];
+      row0s[i] = ftasks[torder[i]].row0;
     }
     int32_t pos = 0;
     for (int i = 0; i < nt; ++i) {  // new contiguous ranges, launch order
@@ -975,49 +777,41 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
               *d_ids = nullptr;
       uint64_t *d_kin = nullptr, *d_kout = nullptr;
       void* d_tmp = nullptr;
-      auto fwd_cleanup = [&]() {
-        dfree(d_starts); dfree(d_ranks); dfree(d_row0s); dfree(d_rl); dfree(d_ids);
-        dfree(d_kin); dfree(d_kout); dfree(d_tmp);
-      };
-#define FWD_TRY(expr)                         \
-  do {                                        \
-    hipError_t _e2 = (expr);                  \
-    if (_e2 != hipSuccess) {                  \
-      fwd_cleanup();                          \
-      PLAN_TRY(_e2);                          \
-    }                                         \
-  } while (0)
-      if (!row_of) {
-        FWD_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
-        hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
-      }
-      FWD_TRY(hipMalloc(&d_starts, sizeof(int32_t) * nt));
-      FWD_TRY(hipMalloc(&d_ranks, sizeof(int32_t) * nt));
-      FWD_TRY(hipMalloc(&d_row0s, sizeof(int32_t) * nt));
-      FWD_TRY(hipMemcpyAsync(d_starts, starts.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s));
-      FWD_TRY(hipMemcpyAsync(d_ranks, ranks.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s));
-      FWD_TRY(hipMemcpyAsync(d_row0s, row0s.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s));
-      FWD_TRY(hipMalloc(&d_rl, sizeof(int32_t) * E));
-      FWD_TRY(hipMalloc(&d_ids, sizeof(int32_t) * E));
-      FWD_TRY(hipMalloc(&d_kin, sizeof(uint64_t) * E));
-      FWD_TRY(hipMalloc(&d_kout, sizeof(uint64_t) * E));
-      FWD_TRY(hipMalloc(&p->fwd_perm, sizeof(int32_t) * E));
-      hipLaunchKernelGGL(fwd_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, row_of, E,
-                         d_starts, d_ranks, d_row0s, nt, cbits, d_kin, d_ids, d_rl);
-      FWD_TRY(hipGetLastError());
-      size_t tb = 0;
-      FWD_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_kin, d_kout, d_ids, p->fwd_perm,
-                                                 (int)E, 0, cbits + tbits, s));
-      FWD_TRY(hipMalloc(&d_tmp, tb));
-      FWD_TRY(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_kin, d_kout, d_ids, p->fwd_perm,
-                                                 (int)E, 0, cbits + tbits, s));
-      FWD_TRY(hipMalloc(&p->fwd_cv, sizeof(uint2) * E));
-      hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->fwd_perm,
-                         idx, d_rl, val, E, p->fwd_cv, true);
-      FWD_TRY(hipGetLastError());
-      FWD_TRY(hipStreamSynchronize(s));
-      fwd_cleanup();
-#undef FWD_TRY
+      const hipError_t fe = [&]() -> hipError_t {
+        hipError_t e = need_row_of();
+        if (e == hipSuccess) e = hipMalloc(&d_starts, sizeof(int32_t) * nt);
+        if (e == hipSuccess) e = hipMalloc(&d_ranks, sizeof(int32_t) * nt);
+        if (e == hipSuccess) e = hipMalloc(&d_row0s, sizeof(int32_t) * nt);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_starts, starts.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_ranks, ranks.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_row0s, row0s.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMalloc(&d_rl, sizeof(int32_t) * E);
+        if (e == hipSuccess) e = hipMalloc(&d_ids, sizeof(int32_t) * E);
+        if (e == hipSuccess) e = hipMalloc(&d_kin, sizeof(uint64_t) * E);
+        if (e == hipSuccess) e = hipMalloc(&d_kout, sizeof(uint64_t) * E);
+        if (e == hipSuccess) e = hipMalloc(&p->fwd_perm, sizeof(int32_t) * E);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(fwd_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, row_of, E,
+                           d_starts, d_ranks, d_row0s, nt, cbits, d_kin, d_ids, d_rl);
+        e = hipGetLastError();
+        size_t tb = 0;
+        if (e == hipSuccess)
+          e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_kin, d_kout, d_ids, p->fwd_perm,
+                                                 (int)E, 0, cbits + tbits, s);
+        if (e == hipSuccess) e = hipMalloc(&d_tmp, tb);
+        if (e == hipSuccess)
+          e = hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_kin, d_kout, d_ids, p->fwd_perm,
+                                                 (int)E, 0, cbits + tbits, s);
+        if (e == hipSuccess) e = hipMalloc(&p->fwd_cv, sizeof(uint2) * E);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->fwd_perm,
+                           idx, d_rl, val, E, p->fwd_cv, true);
+        e = hipGetLastError();
+        return e == hipSuccess ? hipStreamSynchronize(s) : e;
+      }();
+      dfree(d_starts); dfree(d_ranks); dfree(d_row0s); dfree(d_rl); dfree(d_ids);
+      dfree(d_kin); dfree(d_kout); dfree(d_tmp);
+      PLAN_TRY(fe);
       p->device_bytes += (int64_t)E * 12;
     }
     PLAN_TRY(hipMalloc(&p->fwd_tasks, sizeof(FwdTask) * ftasks.size()));
@@ -1034,29 +828,24 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       p->device_bytes += sizeof(int32_t) * ((int64_t)N + 1);
       PLAN_TRY(fwd_fix_stats(p, p->fwd_rowptr, val, s));
     }
-    // Column windows. Default: one launch whose tiles start their column-sorted sweep at the
-    // window a shared clock points to (fwd_rot_ticks per window, about one tile's duration
-    // per full turn), so the tiles running together on an XCD gather from nearby columns
-    // (L2 reuse). fwd_phases > 1 instead runs the windows as separate launches.
-    int B = o.fwd_phases;
-    p->fwd_persistent = o.fwd_persistent ? 1 : 0;
+    // Column windows: one launch whose tiles start their column-sorted sweep at the window a
+    // shared clock points to (fwd_rot_ticks per window, about one tile's duration per full
+    // turn), so the tiles running together on an XCD gather from nearby columns (L2 reuse).
+    int B = 1;
     p->fwd_rot_ticks = 0;
-    if (B <= 1 && o.fwd_rotate != 2 && (k % 4 == 0 || p->fwd_chunk3) && nt > 0) {
+    if (o.fwd_rotate != 2 && (k % 4 == 0 || p->fwd_chunk3)) {
       // the fixed-point kernel sweeps faster: more windows at large k, a higher slot rate
       // (tools/fwd_opts_sweep.py, Reddit: k = 16 1.23 -> 1.19 ms with 260 M edges/s per slot,
       // k = 32 1.81 -> 1.77 with 140 M and 32 windows, k = 64 3.44 -> 3.23 with 64 windows)
       const int Bd = p->fwd_fixed ? (k >= 64 ? 64 : k >= 32 ? 32 : kFwdRotWindows) : kFwdRotWindows;
       B = o.fwd_rot_windows > 0 ? std::min(o.fwd_rot_windows, 64) : Bd;
       // one turn of the clock per tile: the measured per-slot rate scales as ~1/k (Reddit:
-      // 2.4e8, 1.65e8, 0.9e8 edges/s per slot at k = 8, 16, 32; best sweep rates 300, 150-200,
-      // 100 M)
+      // 2.4e8, 1.65e8, 0.9e8 edges/s per slot at k = 8, 16, 32)
       const double rate = o.fwd_rot_rate > 0 ? o.fwd_rot_rate * 1e6
                                              : std::min(5e8, std::max(2e7, (p->fwd_fixed ? kFwdSlotEdgeRateFixed : kFwdSlotEdgeRate) * 16.0 / k));
-      const double tile_edges = (double)E / nt;
-      const double tile_ticks = tile_edges / rate * 1e8;  // s_memrealtime: 100 MHz
+      const double tile_ticks = (double)E / nt / rate * 1e8;  // s_memrealtime: 100 MHz
       p->fwd_rot_ticks = (int)std::max(1.0, tile_ticks / B);
     }
-    if (B == 0) B = 1;
     B = std::max(1, std::min(B, std::max(NC, 1)));
     p->fwd_phases = B;
     PLAN_TRY(hipMalloc(&p->fwd_phase_off, sizeof(int32_t) * nt * (B + 1)));
@@ -1075,19 +864,16 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   // Two tables (no record pack): Reddit k = 32 2.65 -> 2.53 ms, k = 64 4.98 -> 4.92 (k = 16:
   // 1.35 vs 1.39 packed); and where the per-call pack of all NC records costs more than it
   // saves: below kFwdPackMinEdgesPerCol edges per column, or below kFwdPackMinEdgesPerColL2
-  // with an L2-resident selector table (round 3, the pack fused into the statistics pass;
-  // per-rank forward on row shards at k = 16: Reddit W = 8, 62 edges per column and a 3.7 MB
-  // selector table, 0.172 ms packed vs 0.183 two tables, W = 4 (123) 0.757 vs 0.805 ms for
-  // the rank's whole step; ogbn-proteins W = 8, 75 edges per column and 2.1 MB of selectors,
-  // 0.144 packed vs 0.138 two tables; round 2 with a separate pack: Reddit W = 8 0.221
-  // packed vs 0.207). But on a large table, whose gathers mostly miss L2, the record's one line
-  // beats the two tables' two (values + selectors): at k = 16 from tens of MB (yelp, 57 MB:
-  // 0.645 -> 0.54 ms packed; ogbn-products, 196 MB: 4.84 -> 2.95; flickr, 7 MB at 11 edges
-  // per column, stays faster with two tables), at k = 32 only from HBM-sized tables
-  // (ogbn-products 392 MB: 4.95 -> 4.77; yelp 115 MB: 0.67 two tables vs 0.73); never at
-  // k = 64 (ogbn-products 7.08 two tables vs 7.44)
-  const bool big_table = (double)std::max(NC, 1) * 5.0 * k >
-                         (k >= 32 ? kFwdPackedTableBytes : kFwdPackedTableBytes16);
+  // with an L2-resident selector table (per-rank forward on row shards at k = 16: Reddit
+  // W = 8, 62 edges per column and a 3.7 MB selector table, 0.172 ms packed vs 0.183 two
+  // tables, W = 4 (123) 0.757 vs 0.805 ms for the rank's whole step; ogbn-proteins W = 8, 75
+  // edges per column and 2.1 MB of selectors, 0.144 packed vs 0.138 two tables). But on a
+  // large table, whose gathers mostly miss L2, the record's one line beats the two tables'
+  // two (values + selectors): at k = 16 from tens of MB (yelp, 57 MB: 0.645 -> 0.54 ms packed;
+  // ogbn-products, 196 MB: 4.84 -> 2.95; flickr, 7 MB at 11 edges per column, stays faster
+  // with two tables), at k = 32 only from HBM-sized tables (ogbn-products 392 MB: 4.95 ->
+  // 4.77; yelp 115 MB: 0.67 two tables vs 0.73); never at k = 64 (ogbn-products 7.08 two
+  // tables vs 7.44)
   const bool sel_l2 = (double)std::max(NC, 1) * k <= kFwdSelL2Bytes;
   const bool few_edges = E < kFwdPackMinEdgesPerCol * std::max(NC, 1) ||
                          (sel_l2 && E < kFwdPackMinEdgesPerColL2 * std::max(NC, 1));
@@ -1099,15 +885,10 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     // no workspace: the kernel gathers from sp_data / sp_index
   } else if (p->fwd_chunk3 && NC > 0) {
     const int b = (k + 2) / 3 * 16;
-    if (o.fwd_record_bytes != 0 && o.fwd_record_bytes < b) {
-      set_error("maxk_plan_create: fwd_record_bytes too small for the lane-chunk records");
-      return fail(MAXK_ERR_INVALID_ARG);
-    }
-    p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes
-                                          : (b <= 64 ? 64 : b <= 128 ? 128 : b);
+    p->fwd_rec_bytes = b <= 64 ? 64 : b <= 128 ? 128 : b;
     p->fwd_ws_bytes = (int64_t)NC * p->fwd_rec_bytes;
   } else if (k % 4 == 0 && NC > 0) {
-    p->fwd_rec_bytes = o.fwd_record_bytes ? o.fwd_record_bytes : cbsr_record_bytes(k);
+    p->fwd_rec_bytes = cbsr_record_bytes(k);
     p->fwd_ws_bytes = (int64_t)NC * p->fwd_rec_bytes;
   }
   if (p->fwd_fix) {  // the call's {max |x|, min |x|} words after the records
@@ -1120,75 +901,6 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   }
 
   // ---------------- backward
-  // Column blocks of C columns (k f64 accumulators each, <= kBwdLdsBudget of LDS: one
-  // 512-thread work-group per CU); each block's edge range is cut into chunks so that about
-  // 2 x CUs work-groups exist; blocks with several chunks flush with float atomics.
-  int cus = 256;
-  {
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess) {
-      hipDeviceProp_t prop;
-      if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
-        cus = prop.multiProcessorCount;
-    }
-  }
-  const int lds_budget = o.bwd_lds_bytes ? o.bwd_lds_bytes : kBwdLdsBudget;
-  // packed path (sspmm_bwd4_kernel): f32 accumulators, 4 selector slots per lane, grad_out
-  // addressable with 32-bit byte offsets
-  // (or sspmm_bwd1_kernel: one slot per lane, k <= 64 lanes per edge)
-  const bool packed = E > 0 &&
-                      ((k % 4 == 0 && p->bwd_feats == 4) || (k % 2 == 0 && p->bwd_feats == 2 && k / 2 <= kWave) ||
-                       (p->bwd_feats == 1 && k <= kWave)) &&
-                      p->bwd_acc == MAXK_ACC_F32_CAS &&
-                      (uint64_t)N * (uint64_t)D * 4u <= 0xffffffffull;
-  // Slot groups: the k selector slots are split into S groups of k/S consecutive (sorted,
-  // hence clustered) slots, one work-group per (block, group). An edge then touches the
-  // few grad_out lines its group's features fall in, and a block spans S times more
-  // columns, so more edges share each fetched row (SSpMM is bound by L1-miss requests).
-  int S = 1;
-  if (packed && (p->bwd_feats == 4 || p->bwd_feats == 2)) {
-    S = o.bwd_slot_groups ? o.bwd_slot_groups : kBwdSlotGroups;
-    if (o.bwd_slot_groups == 0 && p->bwd_feats == 4 && k >= 32 && k % 8 == 0 && N > 0 && NC > 0) {
-      // k >= 32 with few edges per (block, row): two slot groups, i.e. k/8 lanes per edge and
-      // blocks of twice the columns (Reddit, ~1.9 edges per block row at k = 32: 2.88 ->
-      // 2.66 ms; k = 64, ~1.0: 4.88 -> 4.71; ogbn-proteins k = 64, ~1.9: 3.32 -> 3.25). With
-      // more reuse one group stays faster (ogbn-proteins k = 32, ~3.1: 1.82 vs 1.86).
-      const double c1 = std::min<double>(NC, (lds_budget - 16) / (5.0 * k));
-      if ((double)E / N * c1 / NC < 2.5) S = 2;
-    }
-    while (S > 1 && (k % (p->bwd_feats * S)) != 0) S >>= 1;
-  }
-  p->bwd_slot_groups = S;
-  const int nslots = k / S;
-  // accumulator row stride: nslots + 1 (odd: columns start on different banks) or nslots
-  // 64-bit CAS pairs (sspmm_bwd4_kernel<.., V>): KS even, unpadded by default
-  // (Reddit k = 16: 2.06 -> 1.78 ms; k = 8 1.24 -> 1.16; k = 32 3.21 -> 3.09)
-  p->bwd_cas64 = packed && (p->bwd_feats == 4 || p->bwd_feats == 2) && o.bwd_cas64 != 2;
-  // (Reddit bwd k = 16 1.76 -> 1.70 ms, k = 32 3.08 -> 2.93, k = 64 5.43 -> 4.86; the forward's
-  // 8-B edge words gain nothing: forward only on request)
-  p->bwd_quad = o.quad_loads != 2;
-  // forward quad-shared edge-word loads: with the fixed-point kernel (k = 16 1.19 -> 1.16 ms,
-  // k = 32 1.81 -> 1.78); measured neutral-to-slower on the f64 kernel
-  p->fwd_quad = o.quad_loads == 1 || (o.quad_loads == 0 && p->fwd_fixed);
-  if (p->bwd_cas64) p->bwd_ks = nslots + (o.bwd_acc_pad == 1 ? 4 : 0);
-  else p->bwd_ks = nslots + ((packed && o.bwd_acc_pad == 2) ? 0 : 1);
-  p->bwd_sel_lds = packed && o.bwd_sel_lds != 2 ? 1 : 0;
-  // bytes of LDS per column: accumulators (+ staged selector bytes, nslots per column)
-  const int col_bytes = p->bwd_ks * (int)acc_bytes(p->bwd_acc) + (p->bwd_sel_lds ? nslots : 0);
-  int C = std::max(1, (lds_budget - 16) / col_bytes);
-  C = std::min(C, std::max(NC, 1));
-  // Column-major (CSC) backward, option bwd_algo = 2: one wave per column sums its in-edges
-  // in registers (C = 1: the block sort becomes a column sort). Measured slower than the
-  // column blocks on every graph tried, sparse ones included (ogbn-products k = 32: 17.0 vs
-  // 15.0 ms): a block sweeps its edges in row order, so the work-groups resident together
-  // walk the rows of G in near lock-step and share its lines in L2 and the MALL (PMC: L2 hit
-  // 10-43 % vs 2 % for CSC, 7.0 vs 8.0 L2 misses per edge); a column's in-edges come from
-  // anywhere. Kept as an option for that comparison.
-  const int Lc = k / p->bwd_feats;  // lanes per edge of the column-major kernel
-  const bool csc_ok = E > 0 && p->bwd_feats != 2 && k % p->bwd_feats == 0 && (Lc & (Lc - 1)) == 0 &&
-                      Lc <= kWave &&
-                      (uint64_t)N * (uint64_t)D * 4u <= 0xffffffffull;
-  p->bwd_csc = csc_ok && o.bwd_algo == 2;
   // Two-pass backward (bwd_algo = 3; auto when a column block would see each grad_out row it
   // fetches about once): a row pass stages grad_out[r] in LDS once per row and writes each
   // edge's k products into its slot of an E x k workspace (CSR order), then a column pass
@@ -1216,18 +928,11 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   }
   p->bwd_twopass = twopass;
   p->bwd_tp_rows = R;
-  if (p->bwd_csc || p->bwd_twopass) {
-    C = 1;
-    p->bwd_sel_lds = 0;
-  }
-  const bool colsort = p->bwd_csc || p->bwd_twopass;
-  const bool xcd_order = o.bwd_order == 0 && !colsort;
-  // the column order applies to the packed column-block kernels (their tasks own position
-  // ranges; the column-major kernels sort by the column itself)
-  const int32_t* bcolpos = (colpos && packed && !colsort) ? colpos : nullptr;
-  // row order inside the blocks' streams (column-block kernels; the shared row chunk bounds
-  // need ascending rows): scattered by an affine bijection ra * row + rb mod N
-  const bool row_hash_ok = !colsort && E > 0 && N > 1 && o.bwd_chunk_bounds != 1;
+  if (twopass) C = 1;
+  // the column order applies to the column blocks (the two-pass sorts by the column itself)
+  const int32_t* bcolpos = twopass ? nullptr : colpos;
+  // row order inside the blocks' streams: scattered by an affine bijection ra * row + rb mod N
+  const bool row_hash_ok = !twopass && E > 0 && N > 1;
   bool row_hash = row_hash_ok && o.bwd_row_order == 2;
   int64_t ra = 1, rb = 0;
   int rbits = 1;
@@ -1241,7 +946,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   }
   auto row_pos = [&](int32_t r) -> int64_t { return row_hash ? (ra * (int64_t)r + rb) % N : r; };
   int nblocks = NC > 0 ? (NC + C - 1) / C : 0;
-  if (xcd_order && nblocks >= kXcds) {
+  if (!twopass && nblocks >= kXcds) {
     // a multiple of the XCD count, so every XCD owns the same number of column blocks; and
     // of 8 per XCD when that many blocks are needed anyway (measured: 64 / 128 / 256 blocks
     // for k = 8 / 16 / 32 on Reddit ran 10-25 % faster than 72 / 120 / 240)
@@ -1252,13 +957,10 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   }
   p->bwd_block_cols = C;
   p->n_bwd_blocks = nblocks;
-  std::vector<int64_t> offs(colsort ? 1 : nblocks + 1, 0);
-  p->bwd_row_order = colsort ? 0 : 1;
+  std::vector<int64_t> offs(twopass ? 1 : nblocks + 1, 0);
+  p->bwd_row_order = twopass ? 0 : 1;
   if (E > 0) {
-    if (!row_of) {
-      PLAN_TRY(hipMalloc(&row_of, sizeof(int32_t) * E));
-      hipLaunchKernelGGL(expand_rows_kernel, dim3((N + 3) / 4), dim3(256), 0, s, ptr, N, row_of);
-    }
+    PLAN_TRY(need_row_of());
     PLAN_TRY(hipMalloc(&keys_in, sizeof(uint32_t) * E));
     PLAN_TRY(hipMalloc(&keys_out, sizeof(uint32_t) * E));
     PLAN_TRY(hipMalloc(&ids_in, sizeof(int32_t) * E));
@@ -1276,11 +978,10 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
         hipLaunchKernelGGL(bwd_key_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, E, C, NC,
                            keys_in, ids_in, d_bad, bcolpos);
         hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, ids_in,
-                                               p->bwd_perm, (int)E, 0, end_bit, s);
-        if (e != hipSuccess) return e;
-        e = hipMalloc(&temp, temp_bytes);
+        if (e == hipSuccess)
+          e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys_in, keys_out, ids_in,
+                                                 p->bwd_perm, (int)E, 0, end_bit, s);
+        if (e == hipSuccess) e = hipMalloc(&temp, temp_bytes);
         if (e != hipSuccess) return e;
         return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, ids_in,
                                                   p->bwd_perm, (int)E, 0, end_bit, s);
@@ -1289,26 +990,23 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       uint64_t *k64_in = nullptr, *k64_out = nullptr;
       const hipError_t ke = [&]() -> hipError_t {
         hipError_t e = hipMalloc(&k64_in, sizeof(uint64_t) * E);
-        if (e != hipSuccess) return e;
-        e = hipMalloc(&k64_out, sizeof(uint64_t) * E);
+        if (e == hipSuccess) e = hipMalloc(&k64_out, sizeof(uint64_t) * E);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(bwd_key64_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx, row_of,
                            E, C, NC, k64_in, ids_in, d_bad, bcolpos, ra, rb, N, rbits);
         e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, k64_in, k64_out, ids_in,
-                                               p->bwd_perm, (int)E, 0, end_bit + rbits, s);
-        if (e != hipSuccess) return e;
-        e = hipMalloc(&temp, temp_bytes);
-        if (e != hipSuccess) return e;
-        e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k64_in, k64_out, ids_in,
-                                               p->bwd_perm, (int)E, 0, end_bit + rbits, s);
+        if (e == hipSuccess)
+          e = hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, k64_in, k64_out, ids_in,
+                                                 p->bwd_perm, (int)E, 0, end_bit + rbits, s);
+        if (e == hipSuccess) e = hipMalloc(&temp, temp_bytes);
+        if (e == hipSuccess)
+          e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k64_in, k64_out, ids_in,
+                                                 p->bwd_perm, (int)E, 0, end_bit + rbits, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(key_block_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, k64_out, E,
                            rbits, keys_out);
         e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        return hipStreamSynchronize(s);
+        return e == hipSuccess ? hipStreamSynchronize(s) : e;
       }();
       dfree(k64_in);
       dfree(k64_out);
@@ -1328,16 +1026,13 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
         int nd = 0;
         const hipError_t de = [&]() -> hipError_t {
           hipError_t e = hipMalloc(&d_nd, sizeof(int));
-          if (e != hipSuccess) return e;
-          e = hipMemsetAsync(d_nd, 0, sizeof(int), s);
+          if (e == hipSuccess) e = hipMemsetAsync(d_nd, 0, sizeof(int), s);
           if (e != hipSuccess) return e;
           hipLaunchKernelGGL(dense_window_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s,
                              keys_out, p->bwd_perm, row_of, E, Wn, d_nd);
           e = hipGetLastError();
-          if (e != hipSuccess) return e;
-          e = hipMemcpyAsync(&nd, d_nd, sizeof(int), hipMemcpyDeviceToHost, s);
-          if (e != hipSuccess) return e;
-          return hipStreamSynchronize(s);
+          if (e == hipSuccess) e = hipMemcpyAsync(&nd, d_nd, sizeof(int), hipMemcpyDeviceToHost, s);
+          return e == hipSuccess ? hipStreamSynchronize(s) : e;
         }();
         dfree(d_nd);
         PLAN_TRY(de);
@@ -1347,17 +1042,15 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
         }
       }
     }
-    if (!colsort) p->bwd_row_order = row_hash ? 2 : 1;
-    if (p->bwd_twopass) {
+    if (!twopass) p->bwd_row_order = row_hash ? 2 : 1;
+    if (twopass) {
       PLAN_TRY(hipMalloc(&p->bwd_erec, sizeof(uint32_t) * 2 * (size_t)E));
-      p->bwd_tp_csc = o.bwd_tp_store == 2;
-      // row chunks: the workspace holds one chunk's products (column order: one chunk)
+      // row chunks: the workspace holds one chunk's products
       int P = o.bwd_tp_chunks > 0
                   ? o.bwd_tp_chunks
                   : (int)std::max<int64_t>(1, (int64_t)std::ceil((double)E * k * 4.0 /
                                                                   kBwdTwoPassWorkspaceCap));
       P = std::max(1, std::min(P, std::max(N, 1)));
-      if (p->bwd_tp_csc) P = 1;
       p->bwd_tp_chunks = P;
       p->tp_rows.assign(P + 1, 0);
       p->tp_edges.assign(P + 1, 0);
@@ -1383,49 +1076,38 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       p->device_bytes += (int64_t)E * 12;  // erec + bwd_perm
       hipLaunchKernelGGL(build_erec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, idx,
                          row_of, R, val, E, p->bwd_erec);
-      if (p->bwd_tp_csc) {  // bwd_perm becomes CSR edge -> column-order slot
-        hipLaunchKernelGGL(invert_perm_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
-                           p->bwd_perm, E, ids_in);
-        PLAN_TRY(hipMemcpyAsync(p->bwd_perm, ids_in, sizeof(int32_t) * E,
-                                hipMemcpyDeviceToDevice, s));
-      }
     } else {
-      PLAN_TRY(hipMalloc(&p->bwd_row, sizeof(int32_t) * E));
-      PLAN_TRY(hipMalloc(&p->bwd_col, sizeof(int32_t) * E));
-      PLAN_TRY(hipMalloc(&p->bwd_val, sizeof(float) * E));
-      p->device_bytes += (int64_t)E * 16;
+      PLAN_TRY(hipMalloc(&brow, sizeof(int32_t) * E));
+      PLAN_TRY(hipMalloc(&bcol, sizeof(int32_t) * E));
       hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s,
-                         p->bwd_perm, row_of, idx, val, E, p->bwd_row, p->bwd_col, p->bwd_val,
-                         bcolpos);
+                         p->bwd_perm, row_of, idx, E, brow, bcol, bcolpos);
     }
     PLAN_TRY(hipMalloc(&d_offs, sizeof(int32_t) * (nblocks + 1)));
     hipLaunchKernelGGL(key_offsets_kernel, dim3(nblocks / 256 + 1), dim3(256), 0, s, keys_out,
-                       E, nblocks, reinterpret_cast<int32_t*>(d_offs));
+                       E, nblocks, d_offs);
     PLAN_TRY(hipGetLastError());
     int bad = 0;
     PLAN_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
-    if (colsort) {
+    if (twopass) {
       // column pointers of the column-sorted edge list stay on the device
-      p->bwd_colptr = reinterpret_cast<int32_t*>(d_offs);
+      p->bwd_colptr = d_offs;
       d_offs = nullptr;
       p->device_bytes += sizeof(int32_t) * (nblocks + 1);
-      if (p->bwd_twopass && p->bwd_tp_chunks > 1) {
+      if (p->bwd_tp_chunks > 1) {
         // per-chunk column pointers (rows ascend within a column of the stable sort)
         const int P = p->bwd_tp_chunks;
         int32_t* d_rows = nullptr;
-        PLAN_TRY(hipMalloc(&d_rows, sizeof(int32_t) * (P + 1)));
         const hipError_t ce = [&]() -> hipError_t {
-          hipError_t e = hipMemcpyAsync(d_rows, p->tp_rows.data(), sizeof(int32_t) * (P + 1),
-                                        hipMemcpyHostToDevice, s);
-          if (e != hipSuccess) return e;
-          e = hipMalloc(&p->bwd_colptr2, sizeof(int32_t) * (size_t)(P + 1) * NC);
+          hipError_t e = hipMalloc(&d_rows, sizeof(int32_t) * (P + 1));
+          if (e == hipSuccess) e = hipMemcpyAsync(d_rows, p->tp_rows.data(), sizeof(int32_t) * (P + 1),
+                                                  hipMemcpyHostToDevice, s);
+          if (e == hipSuccess) e = hipMalloc(&p->bwd_colptr2, sizeof(int32_t) * (size_t)(P + 1) * NC);
           if (e != hipSuccess) return e;
           const int64_t n = (int64_t)(P + 1) * NC;
           hipLaunchKernelGGL(tp_colptr_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                              p->bwd_colptr, p->bwd_perm, row_of, NC, d_rows, P, p->bwd_colptr2);
           e = hipGetLastError();
-          if (e != hipSuccess) return e;
-          return hipStreamSynchronize(s);
+          return e == hipSuccess ? hipStreamSynchronize(s) : e;
         }();
         dfree(d_rows);
         PLAN_TRY(ce);
@@ -1444,40 +1126,29 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       return fail(MAXK_ERR_INVALID_ARG);
     }
   }
-  const int64_t target_tasks = (int64_t)(o.bwd_tasks_per_cu ? o.bwd_tasks_per_cu : kBwdTasksPerCu) * cus;
-  const int chunks = (int)std::max<int64_t>(
-      1, (target_tasks + (int64_t)nblocks * S - 1) / std::max<int64_t>((int64_t)nblocks * S, 1));
-  const int64_t min_task_edges = o.bwd_min_task_edges > 0 ? o.bwd_min_task_edges : kBwdMinTaskEdges;
   std::vector<BwdTask> btasks;
   int nshared = 0;
-  if (colsort) {
-    // no tasks: the column-major kernels run one wave per column
-  } else if (xcd_order && E > 0 && nblocks > 0) {
-    // Row-chunk-major, XCD-aware order. Chunk j of a block is the j-th equal share of its
-    // row-sorted edge stream (below), so on graphs without column locality chunk j of every
-    // block covers about the same rows and the work-groups that run together sweep the same
-    // rows of G, sharing its lines in their XCD's L2. Work-groups are dealt round-robin over
-    // the 8 XCDs (blockIdx % 8 labels the work-groups sharing an XCD; speed only, correctness
-    // never depends on it): XCD x owns blocks b = x (mod 8) and walks (chunk, block) in
-    // chunk-major order.
-    // every chunk task clears and flushes its whole block (C * k floats) however few edges
-    // it has: keep >= kBwdMinTaskEdges edges per task (a row shard of a multi-GPU partition
-    // has 1/W of the edges over the same blocks)
-    // ... but not fewer tasks than CUs while those keep >= 4k edges (a row shard of an
-    // 8-GPU partition: 256 tasks of ~56k edges ran 0.24 ms, 512 of ~28k 0.27, 128 0.40; the
-    // own-column part of such a shard, 1.8 M edges over 16 blocks: 16 tasks ran 0.35 ms)
+  if (!twopass && E > 0 && nblocks > 0) {
+    // Task count: about kBwdTasksPerCu work-groups per CU, each of its block's chunks with
+    // >= kBwdMinTaskEdges edges (every chunk clears and stores its whole block, C * k
+    // floats), but not fewer tasks than CUs while those keep >= 4k edges (a row shard of an
+    // 8-GPU partition: 256 tasks of ~56k edges ran 0.24 ms, 512 of ~28k 0.27, 128 0.40)
+    const int64_t target_tasks = (int64_t)(o.bwd_tasks_per_cu ? o.bwd_tasks_per_cu : kBwdTasksPerCu) * cus;
+    const int64_t bS = (int64_t)nblocks * S;
+    const int64_t chunks = std::max<int64_t>(1, (target_tasks + bS - 1) / bS);
+    const int64_t min_task_edges = o.bwd_min_task_edges > 0 ? o.bwd_min_task_edges : kBwdMinTaskEdges;
     int64_t nch64 = std::min<int64_t>(chunks, E / ((int64_t)nblocks * min_task_edges));
-    const int64_t fl = ((int64_t)cus + (int64_t)nblocks * S - 1) / ((int64_t)nblocks * S);
+    const int64_t fl = ((int64_t)cus + bS - 1) / bS;
     if (o.bwd_min_task_edges == 0 && nch64 < fl && E / ((int64_t)nblocks * fl) >= 4096)
       nch64 = std::min<int64_t>(chunks, fl);
     nch64 = std::max<int64_t>(1, nch64);
-    // One 512-thread work-group per CU: a task count just past a multiple of the CUs leaves
-    // the last round mostly idle (ogbn-proteins k = 32: 192 blocks x 3 chunks = 2.25 rounds,
-    // 2.37 ms; x 4 = 3 rounds, 1.82 ms). With the default knobs take the chunk count in
-    // [nch, nch + 2] whose tasks fill their rounds best, keeping >= 0.6 x the minimum task.
+    // One work-group per CU: a task count just past a multiple of the CUs leaves the last
+    // round mostly idle (ogbn-proteins k = 32: 192 blocks x 3 chunks = 2.25 rounds, 2.37 ms;
+    // x 4 = 3 rounds, 1.82 ms). With the default knobs take the chunk count in [nch, nch + 2]
+    // whose tasks fill their rounds best, keeping >= 0.6 x the minimum task.
     if (o.bwd_tasks_per_cu == 0 && o.bwd_min_task_edges == 0) {
       auto fill = [&](int64_t c) {
-        const int64_t t = (int64_t)nblocks * S * c;
+        const int64_t t = bS * c;
         return (double)t / ((double)((t + cus - 1) / cus) * cus);
       };
       int64_t best = nch64;
@@ -1488,151 +1159,30 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       nch64 = best;
     }
     const int nch = (int)nch64;
-    // chunk bounds per block: cbd[b] = {offs[b], ..., offs[b+1]} (nch_b + 1 entries)
-    // default: equal edges (an 8-GPU row shard of Reddit, ~2 chunks per block: 0.227 ms vs
-    // 0.268 with cost bounds, whose per-block chunk counts leave rounds partly idle; the
-    // ID-ordered community graphs that cost bounds were built for are handled by the
-    // scattered row order, with which both run the same: 1.60 / 1.61 ms at k = 16)
-    const int mode = o.bwd_chunk_bounds == 0 ? 2 : o.bwd_chunk_bounds;
-    p->bwd_chunk_mode = mode;
+    // Chunk j of block b holds edges [j, j+1) * nnz_b / nch of the block's row-sorted stream.
+    // On a graph without column locality these are about the same row bounds in every block
+    // (the work-groups that run together sweep the same rows of G); with locality (a
+    // community linking mostly into its own blocks) every task keeps an equal share instead
+    // of a few tasks carrying most of a chunk (41-community Reddit-size graph, k = 16: 3.38
+    // -> 2.18 ms; the scattered row order then takes it to 1.60).
     std::vector<std::vector<int32_t>> cbd((size_t)nblocks);
-    int32_t *d_rb = nullptr, *d_co = nullptr;
-    int64_t *d_cum = nullptr, *d_bc = nullptr, *d_tg = nullptr, *d_lo = nullptr, *d_hi = nullptr;
-    void* d_scan = nullptr;
-    auto chunk_cleanup = [&]() {
-      dfree(d_rb); dfree(d_co); dfree(d_cum); dfree(d_bc); dfree(d_tg); dfree(d_lo); dfree(d_hi);
-      dfree(d_scan);
-      d_rb = d_co = nullptr;
-      d_cum = d_bc = d_tg = d_lo = d_hi = nullptr;
-      d_scan = nullptr;
-    };
-#define CH_TRY(x)                                          \
-    do {                                                   \
-      hipError_t e_ = (x);                                 \
-      if (e_ != hipSuccess) {                              \
-        chunk_cleanup();                                   \
-        PLAN_TRY(e_);                                      \
-      }                                                    \
-    } while (0)
-    if (mode == 1) {
-      // shared row bounds: chunk j of every block covers the same rows [R_j, R_j+1) (equal
-      // edge counts over the whole graph)
-      std::vector<int32_t> co((size_t)nblocks * (nch + 1));
-      std::vector<int32_t> rb(nch + 1);
-      for (int j = 0; j <= nch; ++j) {
-        const int64_t target = E * j / nch;
-        rb[j] = (int32_t)(std::lower_bound(hp.begin(), hp.end(), (int32_t)target) - hp.begin());
-      }
-      rb[0] = 0;
-      rb[nch] = N;
-      CH_TRY(hipMalloc(&d_rb, sizeof(int32_t) * (nch + 1)));
-      CH_TRY(hipMalloc(&d_co, sizeof(int32_t) * co.size()));
-      CH_TRY(hipMemcpyAsync(d_rb, rb.data(), sizeof(int32_t) * (nch + 1), hipMemcpyHostToDevice, s));
-      hipLaunchKernelGGL(chunk_offsets_kernel, dim3((int)((co.size() + 255) / 256)), dim3(256), 0, s,
-                         p->bwd_row, reinterpret_cast<const int32_t*>(d_offs), nblocks, d_rb,
-                         nch + 1, d_co);
-      CH_TRY(hipGetLastError());
-      CH_TRY(hipMemcpyAsync(co.data(), d_co, sizeof(int32_t) * co.size(), hipMemcpyDeviceToHost, s));
-      CH_TRY(hipStreamSynchronize(s));
-      for (int b = 0; b < nblocks; ++b)
-        cbd[b].assign(co.begin() + (size_t)b * (nch + 1), co.begin() + (size_t)(b + 1) * (nch + 1));
-    } else if (mode == 2) {
-      // per-block bounds: chunk j of block b holds edges [j, j+1) * nnz_b / nch of the block's
-      // row-sorted stream. On a graph without column locality these are the shared row
-      // bounds to within a few rows (the work-groups that run together still sweep the same
-      // rows of G); with locality (a community linking mostly into its own blocks) every
-      // task keeps an equal share instead of a few tasks carrying most of a chunk
-      // (41-community Reddit-size graph, k = 16: 3.38 -> 2.18 ms)
-      for (int b = 0; b < nblocks; ++b) {
-        const int64_t o0 = offs[b], nnz = offs[b + 1] - offs[b];
-        cbd[b].resize(nch + 1);
-        for (int j = 0; j <= nch; ++j) cbd[b][j] = (int32_t)(o0 + nnz * j / nch);
-      }
-    } else {
-      // equal cost (bwd_cost_kernel: edges + rc4/4 per (block, row) pair). A task's time
-      // follows the grad_out lines it fetches, once per pair, as much as its edges: with
-      // column locality (an ID-ordered community) a block's stream is a dense run of
-      // community rows (~100 edges per pair) between long sparse stretches (~1 edge per pair),
-      // and equal-edge chunks of it differ several-fold in time. Each block gets chunks in
-      // proportion to its cost (at least nch on average), each chunk an equal share of it.
-      const int rc4 = o.bwd_row_cost ? o.bwd_row_cost : kBwdRowCost4;
-      CH_TRY(hipMalloc(&d_cum, sizeof(int64_t) * E));
-      hipLaunchKernelGGL(bwd_cost_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, keys_out,
-                         p->bwd_row, E, rc4, d_cum);
-      CH_TRY(hipGetLastError());
-      size_t sb = 0;
-      CH_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, sb, d_cum, d_cum, (int)E, s));
-      CH_TRY(hipMalloc(&d_scan, std::max<size_t>(sb, 16)));
-      CH_TRY(hipcub::DeviceScan::InclusiveSum(d_scan, sb, d_cum, d_cum, (int)E, s));
-      CH_TRY(hipMalloc(&d_bc, sizeof(int64_t) * (nblocks + 1)));
-      hipLaunchKernelGGL(block_cost_kernel, dim3(nblocks / 256 + 1), dim3(256), 0, s, d_cum,
-                         reinterpret_cast<const int32_t*>(d_offs), nblocks, d_bc);
-      CH_TRY(hipGetLastError());
-      std::vector<int64_t> bc(nblocks + 1);
-      CH_TRY(hipMemcpyAsync(bc.data(), d_bc, sizeof(int64_t) * (nblocks + 1), hipMemcpyDeviceToHost, s));
-      CH_TRY(hipStreamSynchronize(s));
-      const double tau = std::max(1.0, (double)bc[nblocks] / ((double)nblocks * nch));
-      std::vector<int64_t> tg, lo, hi;
-      std::vector<int32_t> nchb(nblocks);
-      for (int b = 0; b < nblocks; ++b) {
-        const int64_t T = bc[b + 1] - bc[b], nnz = offs[b + 1] - offs[b];
-        // rounded, but no task above 1.25 tau: one work-group per CU runs the tasks in rounds,
-        // so a task count past a multiple of the CUs costs a round (ceil everywhere: Reddit
-        // k = 16 tasks 512 -> ~560), and a block of ~1.5 tau in one chunk stretches one
-        // (rounding alone: an 8-GPU row shard, ~2 chunks per block, 0.244 -> 0.303 ms)
-        int64_t c = std::max<int64_t>({(int64_t)1, (int64_t)std::llround((double)T / tau),
-                                       (int64_t)std::ceil((double)T / (1.25 * tau) - 1e-9)});
-        c = std::min<int64_t>(c, std::max<int64_t>(1, std::min<int64_t>(nnz, 64ll * nch)));
-        nchb[b] = (int32_t)c;
-        for (int64_t j = 1; j < c; ++j) {
-          tg.push_back(bc[b] + (int64_t)((double)T * j / c));
-          lo.push_back(offs[b]);
-          hi.push_back(offs[b + 1]);
-        }
-      }
-      std::vector<int32_t> cut(tg.size());
-      if (!tg.empty()) {
-        const size_t m = tg.size();
-        CH_TRY(hipMalloc(&d_tg, sizeof(int64_t) * m));
-        CH_TRY(hipMalloc(&d_lo, sizeof(int64_t) * m));
-        CH_TRY(hipMalloc(&d_hi, sizeof(int64_t) * m));
-        CH_TRY(hipMalloc(&d_co, sizeof(int32_t) * m));
-        CH_TRY(hipMemcpyAsync(d_tg, tg.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
-        CH_TRY(hipMemcpyAsync(d_lo, lo.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
-        CH_TRY(hipMemcpyAsync(d_hi, hi.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(upper_bound_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
-                           d_cum, d_tg, d_lo, d_hi, (int)m, d_co);
-        CH_TRY(hipGetLastError());
-        CH_TRY(hipMemcpyAsync(cut.data(), d_co, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s));
-        CH_TRY(hipStreamSynchronize(s));
-      }
-      size_t ci = 0;
-      for (int b = 0; b < nblocks; ++b) {
-        cbd[b].push_back((int32_t)offs[b]);
-        for (int j = 1; j < nchb[b]; ++j) cbd[b].push_back(std::max(cbd[b].back(), cut[ci++]));
-        cbd[b].push_back((int32_t)offs[b + 1]);
-      }
+    for (int b = 0; b < nblocks; ++b) {
+      const int64_t o0 = offs[b], nnz = offs[b + 1] - offs[b];
+      cbd[b].resize(nch + 1);
+      for (int j = 0; j <= nch; ++j) cbd[b][j] = (int32_t)(o0 + nnz * j / nch);
     }
-    chunk_cleanup();
-#undef CH_TRY
     // Pieces: a (block, chunk) task holding more than twice the average task's edges is cut
-    // into pieces of equal edge counts (work-groups of their own, in the same chunk-major
-    // slot). The shared row bounds assume edges spread evenly over the blocks; with column
-    // locality (a community of rows linking mostly into its own blocks) a few
-    // tasks would otherwise carry most of a chunk's edges. Cost-balanced chunks need none
-    // (unless bwd_piece_edges asks for them).
+    // into pieces of equal edge counts (work-groups of their own).
     const int64_t avg_task = std::max<int64_t>(1, E / ((int64_t)nblocks * nch));
     const int64_t piece_cap = o.bwd_piece_edges > 0 ? (int64_t)o.bwd_piece_edges
-                              : mode == 3 ? (int64_t)INT32_MAX
-                                          : std::max<int64_t>(2 * avg_task, 16384);
-    const bool slab_flush = packed && o.bwd_flush != 1;
+                                                    : std::max<int64_t>(2 * avg_task, 16384);
+    const bool slab_flush = o.bwd_flush != 1;
     auto npieces = [&](int64_t e) {
       return (int32_t)std::max<int64_t>(1, (e + piece_cap - 1) / piece_cap);
     };
     std::vector<int32_t> pieces_of((size_t)nblocks, 0);
     for (int b = 0; b < nblocks; ++b)
-      for (size_t j = 0; j + 1 < cbd[b].size(); ++j)
-        pieces_of[b] += npieces((int64_t)cbd[b][j + 1] - cbd[b][j]);
+      for (int j = 0; j < nch; ++j) pieces_of[b] += npieces((int64_t)cbd[b][j + 1] - cbd[b][j]);
     // compact slab regions: block b's pieces 1 .. P_b - 1 own C x k floats each
     std::vector<int64_t> slab_base((size_t)nblocks, -1);
     std::vector<int4> comb;
@@ -1653,53 +1203,42 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     }
     // Row-major emission: chunks ordered by the first destination row they sweep (then by
     // block), so the work-groups that run together sweep about the same rows of G and share
-    // its lines in L2. With nch equal-edge chunks per block on a graph without column
-    // locality this is the chunk-major order (chunk j of every block starts near the same
-    // row); with locality it keeps the sparse stretches of different blocks together.
-    std::vector<int32_t> first_row;
+    // its lines in L2; work-group i runs on XCD i % 8 (dealt round-robin; speed only), so
+    // consecutive tasks spread over the XCDs and every XCD gets the same share.
+    std::vector<int32_t> first_row((size_t)nblocks * nch);
     {
       std::vector<int32_t> starts;
       for (int b = 0; b < nblocks; ++b)
-        for (size_t j = 0; j + 1 < cbd[b].size(); ++j)
+        for (int j = 0; j < nch; ++j)
           starts.push_back(std::min<int32_t>(cbd[b][j], (int32_t)std::max<int64_t>(E - 1, 0)));
-      first_row.resize(starts.size());
       int32_t *d_st = nullptr, *d_fr = nullptr;
-      auto fr_cleanup = [&]() { dfree(d_st); dfree(d_fr); };
       const hipError_t fe = [&]() -> hipError_t {
         hipError_t e = hipMalloc(&d_st, sizeof(int32_t) * starts.size());
-        if (e != hipSuccess) return e;
-        e = hipMalloc(&d_fr, sizeof(int32_t) * starts.size());
-        if (e != hipSuccess) return e;
-        e = hipMemcpyAsync(d_st, starts.data(), sizeof(int32_t) * starts.size(),
-                           hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMalloc(&d_fr, sizeof(int32_t) * starts.size());
+        if (e == hipSuccess) e = hipMemcpyAsync(d_st, starts.data(), sizeof(int32_t) * starts.size(),
+                                                hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(gather_i32_kernel, dim3((unsigned)((starts.size() + 255) / 256)),
-                           dim3(256), 0, s, p->bwd_row, d_st, (int)starts.size(), d_fr);
+                           dim3(256), 0, s, brow, d_st, (int)starts.size(), d_fr);
         e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        e = hipMemcpyAsync(first_row.data(), d_fr, sizeof(int32_t) * starts.size(),
-                           hipMemcpyDeviceToHost, s);
-        if (e != hipSuccess) return e;
-        return hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpyAsync(first_row.data(), d_fr, sizeof(int32_t) * starts.size(),
+                                                hipMemcpyDeviceToHost, s);
+        return e == hipSuccess ? hipStreamSynchronize(s) : e;
       }();
-      fr_cleanup();
+      dfree(d_st);
+      dfree(d_fr);
       PLAN_TRY(fe);
     }
     struct ChunkRef { int64_t row; int b, j; };
     std::vector<ChunkRef> order_c;
-    {
-      size_t i = 0;
-      for (int b = 0; b < nblocks; ++b)
-        for (int j = 0; j + 1 < (int)cbd[b].size(); ++j)
-          order_c.push_back(ChunkRef{row_pos(first_row[i++]), b, j});
-    }
+    for (int b = 0; b < nblocks; ++b)
+      for (int j = 0; j < nch; ++j) order_c.push_back(ChunkRef{row_pos(first_row[(size_t)b * nch + j]), b, j});
     std::stable_sort(order_c.begin(), order_c.end(),
                      [](const ChunkRef& a, const ChunkRef& b) { return a.row < b.row; });
     // a block's chunks must come in chunk order (piece numbering, slab regions)
     std::vector<int32_t> next_chunk((size_t)nblocks, 0);
     for (ChunkRef& cr : order_c) cr.j = next_chunk[cr.b]++;
     std::vector<int32_t> next_piece((size_t)nblocks, 0);
-    std::vector<BwdTask> emitted;
     for (const ChunkRef& cr : order_c) {
       const int b = cr.b;
       const int32_t e0 = cbd[b][cr.j], e1 = cbd[b][cr.j + 1];
@@ -1717,11 +1256,11 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
           t.chunk = piece;
           t.slab = (slab_base[b] >= 0 && piece > 0)
                        ? (int32_t)(slab_base[b] + (int64_t)(piece - 1) * C * k) : -1;
-          emitted.push_back(t);
+          btasks.push_back(t);
         }
       }
     }
-    if (slab_flush && !comb.empty()) {
+    if (!comb.empty()) {
       p->bwd_slab_floats = slab_floats;
       p->n_bwd_combine = (int32_t)comb.size();
       PLAN_TRY(hipMalloc(&p->bwd_combine, sizeof(int4) * comb.size()));
@@ -1730,31 +1269,6 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       PLAN_TRY(hipStreamSynchronize(s));
       p->device_bytes += sizeof(int4) * comb.size();
     }
-    // work-group i runs on XCD i % 8 (dealt round-robin; speed only): consecutive tasks of
-    // the emission order spread over the XCDs, and every XCD gets the same share of them
-    btasks = std::move(emitted);
-  } else {
-    for (int b = 0; b < nblocks; ++b) {
-      const int64_t o0 = offs[b], o1 = offs[b + 1];
-      const int64_t nnz = o1 - o0;
-      const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, nnz / min_task_edges));
-      if (nch > 1) ++nshared;
-      for (int i = 0; i < nch; ++i) {
-        for (int g = 0; g < S; ++g) {
-          BwdTask t{};
-          t.col0 = b * C;
-          t.ncols = std::min(C, NC - t.col0);
-          t.e0 = (int32_t)(o0 + nnz * i / nch);
-          t.e1 = (int32_t)(o0 + nnz * (i + 1) / nch);
-          t.shared = nch > 1;
-          t.group = g;
-          btasks.push_back(t);
-        }
-      }
-    }
-    std::stable_sort(btasks.begin(), btasks.end(), [](const BwdTask& a, const BwdTask& b) {
-      return (a.e1 - a.e0) > (b.e1 - b.e0);
-    });
   }
   p->n_bwd_tasks = (int32_t)btasks.size();
   p->n_bwd_shared = nshared;
@@ -1764,51 +1278,31 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
                             hipMemcpyHostToDevice, s));
     p->device_bytes += sizeof(BwdTask) * btasks.size();
   }
-  // packed backward path: records instead of the three parallel arrays
-  if (p->bwd_twopass) {
-    // CSR-order records; bwd_perm (column order -> CSR edge) stays for the column pass
-  } else if (packed || p->bwd_csc) {
+  if (!twopass && E > 0) {
+    // the column blocks' records (padded: a wave may read past the last task's end)
     PLAN_TRY(hipMalloc(&p->bwd_rec, sizeof(uint32_t) * 3 * (size_t)(E + kBwdRecPad)));
     PLAN_TRY(hipMemsetAsync(p->bwd_rec + 3 * E, 0, sizeof(uint32_t) * 3 * kBwdRecPad, s));
-    hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, nullptr,
-                       p->bwd_row, p->bwd_col, p->bwd_val, E, C, D, p->bwd_rec);
+    hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->bwd_perm,
+                       brow, bcol, val, E, C, D, p->bwd_big, p->bwd_rec);
     PLAN_TRY(hipGetLastError());
-    // per-call workspace: lane-ordered selector words (pack_sel_kernel, bwd_feats 4), then
-    // the flush slabs
-    const int64_t sel_bytes = (p->bwd_feats == 4 || p->bwd_feats == 2) ? (int64_t)std::max(NC, 1) * k : 0;
+    // per-call workspace: lane-ordered selector words (kp bytes per column), then the slabs
+    const int64_t sel_bytes = (int64_t)std::max(NC, 1) * p->bwd_kp;
     p->bwd_slab_off = (sel_bytes + 255) / 256 * 256;
-    // flush slabs (bwd_flush 0/2): global float atomics run at ~1.3 TB/s of added bytes and
-    // need a memset grad_sp (an 8-GPU Reddit shard spent ~10 % of its backward there)
-    p->bwd_ws_bytes = p->bwd_slab_floats > 0 ? p->bwd_slab_off + p->bwd_slab_floats * 4
-                                             : sel_bytes;
-    if (p->bwd_ws_bytes > 0 && !p->external_ws)
-      PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)p->bwd_ws_bytes));
-    PLAN_TRY(hipStreamSynchronize(s));
-    dfree(p->bwd_row);
-    dfree(p->bwd_col);
-    dfree(p->bwd_val);
-    p->bwd_row = p->bwd_col = nullptr;
-    p->bwd_val = nullptr;
-    p->device_bytes += (!p->external_ws ? p->bwd_ws_bytes : 0) +
-                       12ll * kBwdRecPad;
+    p->bwd_ws_bytes = p->bwd_slab_floats > 0 ? p->bwd_slab_off + p->bwd_slab_floats * 4 : sel_bytes;
+    if (!p->external_ws) PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)p->bwd_ws_bytes));
+    p->device_bytes += (int64_t)E * 16 + 12ll * kBwdRecPad + (!p->external_ws ? p->bwd_ws_bytes : 0);
   }
   PLAN_TRY(hipStreamSynchronize(s));
-  // the column order stays with the plan when the backward blocks use it
+  // the column order stays with the plan when the column blocks use it
   p->col_order = 1;
-  if (order && bcolpos) p->col_order = order_mode;
   if (order && bcolpos) {
+    p->col_order = order_mode;
     p->bwd_corder = order;
     p->device_bytes += sizeof(int32_t) * (int64_t)NC;
     order = nullptr;
   }
-  drop_order();
-  dfree(row_of);
-  dfree(keys_in);
-  dfree(keys_out);
-  dfree(ids_in);
-  dfree(temp);
-  dfree(d_offs);
-  dfree(d_bad);
+  dfree(order); dfree(colpos); dfree(row_of); dfree(keys_in); dfree(keys_out); dfree(ids_in);
+  dfree(brow); dfree(bcol); dfree(temp); dfree(d_offs); dfree(d_bad);
 #undef PLAN_TRY
   *out_plan = p;
   return MAXK_OK;
@@ -1817,23 +1311,20 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
 extern "C" int maxk_plan_refresh_values(maxk_plan* p, const float* val, void* stream) {
   MAXK_CHECK_ARG(p != nullptr, "maxk_plan_refresh_values: plan is null");
   if (p->num_edges == 0) return MAXK_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int g = grid_for(p->num_edges, 256);
   if (p->bwd_erec)
-    hipLaunchKernelGGL(build_erec_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
-                       (hipStream_t)stream, nullptr, nullptr, 1, val, p->num_edges, p->bwd_erec);
+    hipLaunchKernelGGL(build_erec_kernel, dim3(g), dim3(256), 0, s, nullptr, nullptr, 1, val,
+                       p->num_edges, p->bwd_erec);
   else if (p->bwd_rec)
-    hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
-                       (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
-                       p->bwd_block_cols, p->dim_origin, p->bwd_rec);
-  else
-    hipLaunchKernelGGL(gather_bwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
-                       (hipStream_t)stream, p->bwd_perm, nullptr, nullptr, val, p->num_edges,
-                       nullptr, nullptr, p->bwd_val, nullptr);
+    hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(g), dim3(256), 0, s, p->bwd_perm, nullptr,
+                       nullptr, val, p->num_edges, p->bwd_block_cols, p->dim_origin, p->bwd_big,
+                       p->bwd_rec);
   if (p->fwd_perm)
-    hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(p->num_edges, 256)), dim3(256), 0,
-                       (hipStream_t)stream, p->fwd_perm, nullptr, nullptr, val, p->num_edges,
-                       p->fwd_cv, false);
+    hipLaunchKernelGGL(gather_fwd_kernel, dim3(g), dim3(256), 0, s, p->fwd_perm, nullptr, nullptr,
+                       val, p->num_edges, p->fwd_cv, false);
   if (p->fwd_fix && p->n_fwd_tasks > 0) {
-    const hipError_t e = fwd_fix_stats(p, p->fwd_rowptr, val, (hipStream_t)stream);
+    const hipError_t e = fwd_fix_stats(p, p->fwd_rowptr, val, s);
     if (e != hipSuccess) {
       set_error(std::string("maxk_plan_refresh_values: ") + hipGetErrorString(e));
       return (int)e;
@@ -1852,33 +1343,27 @@ extern "C" int maxk_plan_get_info_sized(const maxk_plan* p, maxk_plan_info* out,
                                         int64_t info_bytes) {
   MAXK_CHECK_ARG(p != nullptr && out != nullptr && info_bytes >= 0,
                  "maxk_plan_get_info: null pointer");
-  maxk_plan_info full{};
-  maxk_plan_info* info = &full;
-  info->num_nodes = p->num_nodes;
-  info->num_cols = p->num_cols;
-  info->num_edges = p->num_edges;
-  info->dim_origin = p->dim_origin;
-  info->dim_k = p->dim_k;
-  info->fwd_tasks = p->n_fwd_tasks;
-  info->fwd_split_rows = p->n_zero_rows;
-  info->bwd_block_cols = p->bwd_block_cols;
-  info->bwd_blocks = p->n_bwd_blocks;
-  info->bwd_tasks = p->n_bwd_tasks;
-  info->bwd_shared_blocks = p->n_bwd_shared;
-  info->device_bytes = p->device_bytes;
-  info->bwd_algo = p->bwd_twopass ? 3 : p->bwd_csc ? 2 : 1;
-  info->col_order = p->col_order;
-  info->bwd_chunk_bounds = (p->bwd_twopass || p->bwd_csc) ? 0 : p->bwd_chunk_mode;
-  info->bwd_tp_chunks = p->bwd_twopass ? p->bwd_tp_chunks : 1;
-  info->bwd_row_order = p->bwd_row_order;
-  info->bwd_workspace_peak = p->bwd_ws_bytes;
-  std::memcpy(out, info, (size_t)std::min<int64_t>(info_bytes, (int64_t)sizeof(maxk_plan_info)));
+  maxk_plan_info info{};
+  info.num_nodes = p->num_nodes;
+  info.num_cols = p->num_cols;
+  info.num_edges = p->num_edges;
+  info.dim_origin = p->dim_origin;
+  info.dim_k = p->dim_k;
+  info.fwd_tasks = p->n_fwd_tasks;
+  info.fwd_split_rows = p->n_zero_rows;
+  info.bwd_block_cols = p->bwd_block_cols;
+  info.bwd_blocks = p->n_bwd_blocks;
+  info.bwd_tasks = p->n_bwd_tasks;
+  info.bwd_shared_blocks = p->n_bwd_shared;
+  info.device_bytes = p->device_bytes;
+  info.bwd_algo = p->bwd_twopass ? MAXK_BWD_TWO_PASS : MAXK_BWD_COLUMN_BLOCKS;
+  info.col_order = p->col_order;
+  info.bwd_chunk_bounds = p->bwd_twopass ? 0 : 2;
+  info.bwd_tp_chunks = p->bwd_twopass ? p->bwd_tp_chunks : 1;
+  info.bwd_row_order = p->bwd_row_order;
+  info.bwd_workspace_peak = p->bwd_ws_bytes;
+  std::memcpy(out, &info, (size_t)std::min<int64_t>(info_bytes, (int64_t)sizeof(maxk_plan_info)));
   return MAXK_OK;
-}
-
-__global__ void iota_kernel(int n, int32_t* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = i;
 }
 
 extern "C" int maxk_plan_get_col_order(const maxk_plan* p, int32_t* order, void* stream) {

@@ -13,17 +13,18 @@
 //   forward : a 256-thread work-group owns <= 32 whole destination rows (LDS accumulator
 //             rows x D); its edges are processed flat, k/4 lanes per edge, 4 features per
 //             lane (one dwordx4 value gather + one dword selector gather; or lane chunks of
-//             3 values + their selectors for k % 16 != 0), U independent sub-steps in
-//             flight per wave; products are accumulated in LDS with f64 atomics
-//             (ds_add_f64, ~9x the f32 rate), and the rows are written back once with
-//             coalesced dwordx4 stores. Only rows longer than the task cap are split, and
-//             only those touch global atomics.
-//   backward: a 512-thread work-group owns a block of source columns whose k-wide
+//             3 values + their selectors for k % 16 != 0), 8 independent sub-steps in
+//             flight per wave; products are accumulated in LDS in exact fixed point
+//             (ds_add_u64, LdsFix) or f64 (ds_add_f64), and the rows are written back once
+//             with coalesced dwordx4 stores. Only rows longer than the task cap are split,
+//             and only those touch global atomics.
+//   backward: a 512/768-thread work-group owns a block of source columns whose k-wide
 //             gradients live in LDS; it sweeps the block's edges in destination-row order
 //             (plan-built block-major edge list), so the lanes of one instruction gather
 //             from few rows of grad_out (L1 reuse); updates are 64-bit compare-and-swaps on
-//             float pairs; the block is stored (or atomically flushed when it is split over
-//             several work-groups) once at the end.
+//             float pairs; the block is stored once at the end (or, split over several
+//             work-groups, into slabs that one combine pass adds in a fixed order). Graphs
+//             whose column blocks see each grad_out row about once use a two-pass form.
 #include <algorithm>
 #include <type_traits>
 
@@ -31,55 +32,38 @@
 
 namespace maxk {
 
-// Accumulator kinds: MAXK_ACC_F64 (double, ds_add_f64) and MAXK_ACC_F32_CAS (float,
-// ds_read + ds_cmpst_rtn_b32 loop: the integer CAS path runs at the f64-atomic rate).
-template <int ACC>
-struct LdsAcc;
-
 // Quad-shared loads: the L lanes of an edge (L % 4 == 0, quad-aligned) need the same edge
-// record; each lane loads ONE dword of it and quad_perm DPP moves broadcast the words, so
-// the texture path returns 4 B per lane instead of the whole record per lane (PMC: TD busy
-// ~93 % in both kernels, the record/edge-word loads were a third of its bytes).
+// record; lane q of a quad loads the record of sub-step 4j + q and quad_perm DPP moves
+// broadcast it, so one load instruction serves four sub-steps.
 template <int W>
 __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
   static_assert(W >= 0 && W < 4, "quad lane");
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, W * 0x55, 0xf, 0xf, false);
 }
 
+__device__ __forceinline__ uint32_t quad_pick(uint32_t v, int u) {
+  switch (u & 3) {
+    case 0: return quad_bcast<0>(v);
+    case 1: return quad_bcast<1>(v);
+    case 2: return quad_bcast<2>(v);
+    default: return quad_bcast<3>(v);
+  }
+}
 
-// add(p, v): one accumulated term. The forward's edge loop uses scale(val, sc) once per edge
-// and add2(p, scaled val, x) per slot, so the fixed-point accumulator below can fold the scale
-// and the rounding into one fma.
-template <>
-struct LdsAcc<MAXK_ACC_F64> {
+// Forward f64 accumulator: ds_add_f64 of the f32 product val * x. Inputs with non-finite
+// values take this path, so its idle lanes add 0 * 0 (fwd_edges4 zeroes their values).
+struct LdsF64 {
   using T = double;
   using V = float;
-  static __device__ __forceinline__ void add(double* p, float v) {
-    lds_add(p, (double)v);
-  }
+  static constexpr bool kFixed = false;
   static __device__ __forceinline__ V scale(float v, double) { return v; }
-  static __device__ __forceinline__ void add2(double* p, float v, float x) { add(p, v * x); }
-};
-
-template <>
-struct LdsAcc<MAXK_ACC_F32_CAS> {
-  using T = float;
-  using V = float;
-  static __device__ __forceinline__ void add(float* p, float v) {
-    unsigned* u = reinterpret_cast<unsigned*>(p);
-    unsigned old = *u;
-    while (true) {
-      const unsigned assumed = old;
-      old = atomicCAS(u, assumed, __float_as_uint(__uint_as_float(assumed) + v));
-      if (old == assumed) break;
-    }
+  static __device__ __forceinline__ void add2(double* p, float v, float x) {
+    lds_add(p, (double)(v * x));
   }
-  static __device__ __forceinline__ V scale(float v, double) { return v; }
-  static __device__ __forceinline__ void add2(float* p, float v, float x) { add(p, v * x); }
 };
 
 // Forward fixed-point accumulator (plan->fwd_fixed): ds_add_u64 runs at ~1.9x the ds_add_f64
-// rate, and the f64 atomic bounds the forward at k >= 32 (tools/probe_fwd_build.py: Reddit
+// rate, and the f64 atomic bounds the forward at k >= 32 (profiles/r02/fwd_probe/lds_update_probes.jsonl: Reddit
 // k = 32 2.46 -> 1.74 ms, k = 64 4.79 -> 3.34 with the integer atomic). A term val * x is
 // scaled by 2^s (per task and call, fwd_fix_scale) and rounded to an integer by ONE fma with
 // M = 1.5 * 2^52: r = fma(val * 2^s, x, M) lies in [2^52, 2^53) while |term| < 2^51, where the
@@ -91,6 +75,7 @@ struct LdsAcc<MAXK_ACC_F32_CAS> {
 struct LdsFix {
   using T = unsigned long long;
   using V = double;
+  static constexpr bool kFixed = true;
   static __device__ __forceinline__ V scale(float v, double sc) { return (double)v * sc; }
   static __device__ __forceinline__ void add2(T* p, double v, float x) {
     const double r = __builtin_fma(v, (double)x, 0x1.8p52);
@@ -133,16 +118,17 @@ __device__ __forceinline__ double fwd_fix_scale(int2 fix, const uint32_t* xs, in
   return __builtin_ldexp(1.0, sc);
 }
 
-// cbsr_stats_kernel for k % 4 == 0 (k <= 256): L = k/4 lanes per row, each loading its 4
+// cbsr_stats4_kernel for k % 4 == 0 (k <= 256): L = k/4 lanes per row, each loading its 4
 // values (float4) and their 4 selectors (one dword), rows 64/L per wave, coalesced. Per row,
 // inclusive prefix scans over its L lanes (shuffles) give the sum of |x|, the max |x|, and
 // whether a lane's first nonzero selector is <= the last nonzero selector of any earlier lane
 // (or its own nonzero selectors do not ascend): the same bound as the thread-per-row kernel
 // below, with the row sum added in another order (its 2^-10 headroom covers that).
 //
-// PACK: the same pass also writes the forward's packed CBSR records (pack_cbsr_kernel's
-// layout: k values, then the k selector bytes, rec_bytes per row), so the per-call pack and
-// the statistics cost one read of the tables. STATS = false: the pack alone.
+// PACK: the same pass also writes the forward's packed CBSR records (k values, then the k
+// selector bytes, rec_bytes per row), so the per-call pack and the statistics cost one read
+// of the tables. STATS = false: the pack alone. The forward's split rows (summed atomically
+// by their segments) are zeroed here too, one launch before the forward.
 template <bool PACK, bool STATS>
 __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restrict__ x,
                                                           const uint8_t* __restrict__ sel,
@@ -150,10 +136,9 @@ __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restric
                                                           uint32_t* st1, uint8_t* __restrict__ rec,
                                                           int rec_bytes,
                                                           const int32_t* __restrict__ zrows,
-                                                          int nz, float* __restrict__ out, int D) {
+                                                          int nz, float* __restrict__ out, int D,
+                                                          int ds, int is) {
   __shared__ uint32_t smx[256 / kWave], smn[256 / kWave];
-  // the forward's split rows (summed atomically by their segments) start from zero: zeroed
-  // here, one launch before the forward, instead of by a zero_rows_kernel launch of their own
   for (int i = blockIdx.x; i < nz; i += gridDim.x)
     for (int t = threadIdx.x; t < D; t += blockDim.x) out[(size_t)zrows[i] * D + t] = 0.f;
   const int L = k >> 2;
@@ -170,8 +155,8 @@ __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restric
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t s = 0u;
     if (live) {
-      v = *reinterpret_cast<const float4*>(x + r * k + 4 * q);
-      s = *reinterpret_cast<const uint32_t*>(sel + r * k + 4 * q);
+      v = *reinterpret_cast<const float4*>(x + r * ds + 4 * q);
+      s = *reinterpret_cast<const uint32_t*>(sel + r * is + 4 * q);
       if constexpr (PACK) {
         uint8_t* rp = rec + r * rec_bytes;
         *reinterpret_cast<float4*>(rp + 16 * q) = v;
@@ -250,12 +235,11 @@ __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restric
 // headroom for the f32 sum): m nonzero entries on one selector add m terms to one LDS slot
 // (maxk_hip.h: repeated selectors are summed), which a max |x| bound would not cover. Zero
 // entries (ref_compat padding) add nothing and are skipped. Both words are zeroed before the
-// launch; a few hundred work-groups reduce in LDS and add one atomic each per word (one
-// atomic per wave on a shared word cost ~190 us at k = 16).
+// launch; a few hundred work-groups reduce in LDS and add one atomic each per word.
 __global__ __launch_bounds__(256) void cbsr_stats_kernel(const float* __restrict__ x,
                                                          const uint8_t* __restrict__ sel,
                                                          int64_t nrows, int k, uint32_t* st0,
-                                                         uint32_t* st1) {
+                                                         uint32_t* st1, int ds, int is) {
   __shared__ uint32_t smx[256 / kWave], smn[256 / kWave];
   uint32_t mx = 0u, mn = 0x7fffffffu;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows;
@@ -264,28 +248,17 @@ __global__ __launch_bounds__(256) void cbsr_stats_kernel(const float* __restrict
     float sum = 0.f;
     int prev = -1;
     bool rep = false;
-    auto take = [&](float v, int s) {
-      const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
-      if (b == 0u) return;
+    const float* xr = x + r * ds;
+    const uint8_t* sr = sel + r * is;
+    for (int l = 0; l < k; ++l) {
+      const uint32_t b = __float_as_uint(xr[l]) & 0x7fffffffu;
+      if (b == 0u) continue;
+      const int s = sr[l];
       mb = max(mb, b);
       lo = min(lo, b);
       sum += __uint_as_float(b);
       rep = rep || s <= prev;
       prev = s;
-    };
-    const float* xr = x + r * k;
-    const uint8_t* sr = sel + r * k;
-    if ((k & 3) == 0) {
-      for (int l = 0; l < k; l += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(xr + l);
-        const uint32_t s = *reinterpret_cast<const uint32_t*>(sr + l);
-        take(v.x, s & 0xffu);
-        take(v.y, (s >> 8) & 0xffu);
-        take(v.z, (s >> 16) & 0xffu);
-        take(v.w, s >> 24);
-      }
-    } else {
-      for (int l = 0; l < k; ++l) take(xr[l], sr[l]);
     }
     // a non-finite sum (or value) gives bits >= 0x7f800000: fwd_fix_scale falls back
     const uint32_t rb = rep ? max(mb, __float_as_uint(sum * (1.0f + 0x1p-10f)) & 0x7fffffffu) : mb;
@@ -319,11 +292,11 @@ __global__ __launch_bounds__(256) void cbsr_stats_kernel(const float* __restrict
 // Lane-chunk CBSR records (plan->fwd_chunk3): chunk j of column c is 16 B, {x[3j],
 // x[3j+1], x[3j+2], selectors 3j..3j+2 in bytes 0..2 of the 4th word}, so ONE dwordx4 gather
 // gives a lane its 3 values and their selectors (the 4-values-per-lane records need a
-// second, selector, gather per lane). The gathers are bound by L1 line lookups per
-// instruction, not by bytes (tools/ubench_tcp.hip); padding slots (3j+i >= k) are 0.
+// second, selector, gather per lane). Padding slots (3j+i >= k) are 0.
 __global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
                                   const uint8_t* __restrict__ sp_index,
-                                  uint8_t* __restrict__ rec, int ncols, int k, int rec_bytes) {
+                                  uint8_t* __restrict__ rec, int ncols, int k, int rec_bytes,
+                                  int ds, int is) {
   const int chunks = (k + 2) / 3;
   const int64_t total = (int64_t)ncols * chunks;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -335,90 +308,62 @@ __global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
     for (int i = 0; i < 3; ++i) {
       const int l = 3 * j + i;
       if (l < k) {
-        w[i] = __float_as_uint(sp_data[c * k + l]);
-        w[3] |= (uint32_t)sp_index[c * k + l] << (8 * i);
+        w[i] = __float_as_uint(sp_data[c * ds + l]);
+        w[3] |= (uint32_t)sp_index[c * is + l] << (8 * i);
       }
     }
     *reinterpret_cast<uint4*>(rec + c * rec_bytes + j * 16) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
-// One wave's share of the forward edges [e0, e1) (VEC = 4 lanes path): U sub-steps per
-// iteration with every load issued before the first LDS update. The chain (col, val) ->
-// CBSR record -> LDS has two dependent global round trips, so memory-level parallelism
-// comes from U independent sub-steps per wave. Out-of-range lanes load a clamped (valid)
-// edge and skip the update. PF: the next iteration's edge words are loaded right after
-// this iteration's record gathers (loads retire in issue order), so the edge stream's HBM
-// latency overlaps the LDS updates.
-// FL bit 0 (kFwdFlagPrefetch): prefetch; bit 1 (kFwdFlagBranchless): idle lanes add 0 instead
-// of branching; bit 2 (kFwdFlagChunk3): lane-chunk records (pack_cbsr3_kernel), l0 = chunk.
-template <int U, class A, int FL>
+// One wave's share of the forward edges [e0, e1) (4 features per lane, or lane chunks):
+// U = kFwdUnroll sub-steps per iteration with every load issued before the first LDS update.
+// The chain (col, val) -> CBSR record -> LDS has two dependent global round trips, so
+// memory-level parallelism comes from U independent sub-steps per wave. Idle lanes load a
+// clamped (valid) edge and add 0 at its addresses instead of branching (with a branch the
+// compiler sinks sub-step 0's gather below the other loads).
+// FL kFwdFlagChunk3: lane-chunk records (pack_cbsr3_kernel), l0 = chunk. kFwdFlagQuad (L % 4
+// == 0): edge-major windows, sub-step u of slot s takes edge base + s U + u, so lane q of a
+// quad loads the whole edge word of sub-step 4j + q (the quad reads 32 contiguous bytes) and
+// DPP hands it to the quad: one edge-word instruction per four sub-steps.
+// (Batching the selector words the same way, 64 scattered records per instruction, ran k = 16
+// 1.10 -> 1.48 ms: only contiguous loads gain from fewer instructions.)
+template <class A, int FL>
 __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, int wave,
                                            int nwaves, int EPS, int slot, int l0, bool lane_on,
                                            const uint2* __restrict__ cv,
                                            const uint8_t* __restrict__ rec, int rec_bytes,
-                                           const uint8_t* __restrict__ seltab, int D, int k,
-                                           double sc) {
+                                           const uint8_t* __restrict__ seltab, int ss, int D,
+                                           int k, double sc) {
   using T = typename A::T;
-  constexpr bool PF = (FL & kFwdFlagPrefetch) != 0;
+  constexpr int U = kFwdUnroll;
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
-  constexpr bool QL = (FL & kFwdFlagQuad) != 0;  // L % 4 == 0: lanes load one word each
+  constexpr bool EM = (FL & kFwdFlagQuad) != 0;
   const int last = e1 - 1;
-  const uint32_t* cvw = reinterpret_cast<const uint32_t*>(cv) + (threadIdx.x & 1);
-  auto load_cv = [&](int e) -> uint2 {
-    if constexpr (QL) return make_uint2(cvw[2 * (size_t)e], 0u);
-    else return cv[e];
-  };
-  auto split_cv = [&](uint2 w, uint32_t& c, float& v) {
-    if constexpr (QL) {
-      c = quad_bcast<0>(w.x);
-      v = __uint_as_float(quad_bcast<1>(w.x));
-    } else {
-      c = w.x;
-      v = __uint_as_float(w.y);
-    }
-  };
   const int stride = nwaves * EPS * U;
-  int base = e0 + wave * EPS * U;
-  uint2 wn[U];
-  if (PF) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) wn[u] = load_cv(min(base + u * EPS + slot, last));
-  }
-  // Edge-major windows (quad loads without prefetch, U % 4 == 0): sub-step u of slot s takes
-  // edge base + s U + u, so lane q of a quad loads the whole edge word of sub-step 4j + q
-  // (the quad reads 32 contiguous bytes) and DPP hands it to the quad: one edge-word
-  // instruction per four sub-steps instead of one per sub-step
-  // (Batching the selector words the same way, 64 scattered records per instruction, ran k = 16
-  // 1.10 -> 1.48 ms: only contiguous loads gain from fewer instructions.)
-  constexpr bool EM = QL && !PF && (U % 4) == 0;
-  for (; base < e1; base += stride) {  // D: the accumulator's row stride
+  const int qq = threadIdx.x & 3;
+  for (int base = e0 + wave * EPS * U; base < e1; base += stride) {
     uint32_t cw[U];
     float v[U];
     bool ok[U];
     if constexpr (EM) {
-      const int qq = threadIdx.x & 3;
       uint2 wq[U / 4];
 #pragma unroll
       for (int j = 0; j < U / 4; ++j) wq[j] = cv[min(base + slot * U + 4 * j + qq, last)];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = base + slot * U + u;
-        ok[u] = lane_on && e < e1;
-        const uint2 w = wq[u / 4];
-        switch (u & 3) {
-          case 0: cw[u] = quad_bcast<0>(w.x); v[u] = __uint_as_float(quad_bcast<0>(w.y)); break;
-          case 1: cw[u] = quad_bcast<1>(w.x); v[u] = __uint_as_float(quad_bcast<1>(w.y)); break;
-          case 2: cw[u] = quad_bcast<2>(w.x); v[u] = __uint_as_float(quad_bcast<2>(w.y)); break;
-          default: cw[u] = quad_bcast<3>(w.x); v[u] = __uint_as_float(quad_bcast<3>(w.y)); break;
-        }
+        ok[u] = lane_on && base + slot * U + u < e1;
+        cw[u] = quad_pick(wq[u / 4].x, u);
+        v[u] = __uint_as_float(quad_pick(wq[u / 4].y, u));
       }
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = base + u * EPS + slot;
         ok[u] = lane_on && e < e1;
-        split_cv(PF ? wn[u] : load_cv(ok[u] ? e : last), cw[u], v[u]);
+        const uint2 w = cv[ok[u] ? e : last];
+        cw[u] = w.x;
+        v[u] = __uint_as_float(w.y);
       }
     }
     float4 x[U];
@@ -433,112 +378,92 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
       } else {
         x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
         // two tables (plan->fwd_two_tables): values straight from sp_data, selectors from
-        // sp_index (no per-call pack); else the selector word of the packed record
-        const uint8_t* sp = seltab ? seltab + (size_t)(cw[u] & kFwdColMask) * k + l0
+        // sp_index (no per-call pack); else the selector word of the record (packed per call,
+        // or the caller's interleaved records)
+        const uint8_t* sp = seltab ? seltab + (size_t)(cw[u] & kFwdColMask) * ss + l0
                                    : rp + 4 * k + l0;
         sel[u] = *reinterpret_cast<const uint32_t*>(sp);
       }
     }
-    if (PF) {  // unconditional (clamped), see sspmm_bwd4_kernel
-      __builtin_amdgcn_sched_barrier(0);  // keep every gather ahead of these loads
+    if constexpr (!A::kFixed) {  // finite-only fixed point: 0 * x is 0 there
 #pragma unroll
-      for (int u = 0; u < U; ++u) wn[u] = load_cv(min(base + stride + u * EPS + slot, last));
-      __builtin_amdgcn_sched_barrier(0);
+      for (int u = 0; u < U; ++u)
+        if (!ok[u]) x[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    // Branchless: idle lanes add 0 at their clamped (valid) edge's addresses; with a branch
-    // the compiler sinks sub-step 0's gather below the other loads (measured: faster at
-    // k = 16, slower at k = 8).
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if ((FL & kFwdFlagBranchless) || ok[u]) {
-        T* arow = acc + (cw[u] >> kFwdColBits) * D;
-        const uint32_t sv = sel[u];
-        const typename A::V vu = A::scale((FL & kFwdFlagBranchless) && !ok[u] ? 0.f : v[u], sc);
-        if constexpr (C3) {
-          // l0 = chunk index: slots 3 l0 .. 3 l0 + 2 (the last chunk may be partly padding)
-          A::add2(arow + (sv & 0xffu), vu, x[u].x);
-          if (3 * l0 + 1 < k) A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
-          if (3 * l0 + 2 < k) A::add2(arow + ((sv >> 16) & 0xffu), vu, x[u].z);
-        } else {
-          A::add2(arow + (sv & 0xffu), vu, x[u].x);
-          A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
-          A::add2(arow + ((sv >> 16) & 0xffu), vu, x[u].z);
-          A::add2(arow + (sv >> 24), vu, x[u].w);
-        }
+      T* arow = acc + (cw[u] >> kFwdColBits) * D;
+      const uint32_t sv = sel[u];
+      const typename A::V vu = A::scale(ok[u] ? v[u] : 0.f, sc);
+      if constexpr (C3) {
+        // l0 = chunk index: slots 3 l0 .. 3 l0 + 2 (the last chunk may be partly padding)
+        A::add2(arow + (sv & 0xffu), vu, x[u].x);
+        if (3 * l0 + 1 < k) A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
+        if (3 * l0 + 2 < k) A::add2(arow + ((sv >> 16) & 0xffu), vu, x[u].z);
+      } else {
+        A::add2(arow + (sv & 0xffu), vu, x[u].x);
+        A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
+        A::add2(arow + ((sv >> 16) & 0xffu), vu, x[u].z);
+        A::add2(arow + (sv >> 24), vu, x[u].w);
       }
     }
   }
 }
 
-// Column phases: all work-groups of one launch gather from the same 1/B of the CBSR table
-// (phase b = source columns [b*NC/B, (b+1)*NC/B)), so the records they touch stay in L2
-// (tools/ubench_gather.hip: ~300 vs ~63 G edges/s for a shared window vs the whole table).
-// Phase 0 stores the task's rows, later phases continue from the stored partial sums.
-template <int VEC, int ACC, int U, int NT, int FL>
-__global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
-    const FwdTask* __restrict__ tasks, int ntasks, const int32_t* __restrict__ phase_off,
-    int phases, int phase, const uint2* __restrict__ cv,
-    const float* __restrict__ sp_data, const uint8_t* __restrict__ sp_index,
-    const uint8_t* __restrict__ rec, int rec_bytes, float* __restrict__ out, int D, int k,
-    int tile_rows, int rot_ticks, const uint8_t* __restrict__ seltab, int accum,
-    const int2* __restrict__ fix_tab, const uint32_t* __restrict__ xstat, int xs_n,
-    int xs_stride, int xs_off2) {
-  using A = LdsAcc<ACC>;
-  using T = typename A::T;
+// Work-group = one task (FwdTask: whole rows, or one segment of a long row). Its edges are
+// column-sorted; rot_ticks > 0: the sweep starts at the column window the shared 100 MHz clock
+// points to and wraps around, so concurrently running tiles gather from the same columns (L2
+// reuse). accum: the rows of out hold a prior sum to add to (the multi-GPU split's remote
+// part). VEC == 1: k % 4 != 0 beyond the lane chunks' range (k > 192), min(k, 64) lanes per
+// edge looping over the row's k entries, f64 atomics.
+template <int VEC, int FL>
+__global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
+    const FwdTask* __restrict__ tasks, const int32_t* __restrict__ phase_off, int phases,
+    const uint2* __restrict__ cv, const float* __restrict__ sp_data,
+    const uint8_t* __restrict__ sp_index, const uint8_t* __restrict__ rec, int rec_bytes,
+    float* __restrict__ out, int D, int k, int rot_ticks, const uint8_t* __restrict__ seltab,
+    int ss, int ds, int accum, const int2* __restrict__ fix_tab,
+    const uint32_t* __restrict__ xstat, int xs_n, int xs_stride, int xs_off2) {
   extern __shared__ __align__(16) double smem_d[];
-  T* acc = reinterpret_cast<T*>(smem_d);
-  // Work-group w runs tasks w, w + G, ... (G = grid size; G = #tasks by default, or the
-  // resident capacity with the fwd_persistent option, which measured slower on Reddit).
-  // rot_ticks > 0: one launch, each task's sweep rotated to start at the window of the
-  // shared 100 MHz clock, so concurrently running tiles gather from the same columns.
-  for (int ti = blockIdx.x; ti < ntasks; ti += gridDim.x) {
-  FwdTask t = tasks[ti];
-  int emid = -1;
+  double* acc = smem_d;
+  unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(smem_d);
   __shared__ int s_w0;
+  const int ti = blockIdx.x;
+  FwdTask t = tasks[ti];
+  t.e0 = phase_off[ti * (phases + 1)];
+  t.e1 = phase_off[ti * (phases + 1) + phases];
+  int emid = -1;
   if (rot_ticks > 0) {
-    // start the column-sorted sweep at the window the clock points to, wrapping around
-    // (read once per work-group: every wave must split the task at the same edge)
-    __syncthreads();
+    // read once per work-group: every wave must split the task at the same edge
     if (threadIdx.x == 0)
       s_w0 = (int)((__builtin_amdgcn_s_memrealtime() / (uint64_t)rot_ticks) % (uint64_t)phases);
     __syncthreads();
-    const int w0 = s_w0;
-    t.e0 = phase_off[ti * (phases + 1)];
-    t.e1 = phase_off[ti * (phases + 1) + phases];
-    emid = phase_off[ti * (phases + 1) + w0];
-  } else {
-  t.e0 = phase_off[ti * (phases + 1) + phase];
-  t.e1 = phase_off[ti * (phases + 1) + phase + 1];
+    emid = phase_off[ti * (phases + 1) + s_w0];
   }
-  const bool cont = phase > 0 || accum;  // rows of out hold a prior sum to add to
-  if (cont && t.e0 == t.e1) continue;  // nothing to add (uniform)
+  if (accum && t.e0 == t.e1) return;  // nothing to add (uniform)
   // fixed-point accumulation for this task (LdsFix), else f64; the 8-byte slots are the same.
   // A continuing launch in fixed point sums its own terms from zero and adds the prior f32
-  // row at the write-back (one more f32 rounding, as a column phase of the reference would)
+  // row at the write-back (one more f32 rounding)
   double fsc = 0.0;
-  if constexpr (VEC == 4 && ACC == MAXK_ACC_F64) {
+  if constexpr (VEC == 4) {
     if (fix_tab) fsc = fwd_fix_scale(fix_tab[ti], xstat, xs_n, xs_stride, xs_off2);
   }
   const bool fixed = fsc != 0.0;
-  unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(smem_d);
   const bool split = t.nrows < 0;
   const int nrows = split ? 1 : t.nrows;
   const int n = nrows * D;
   const int DS = D + kFwdRowPad;  // LDS row stride (elements)
-  __syncthreads();  // the previous task's write-back has finished reading acc
-  if (cont && !split && !fixed) {  // continue from the stored rows
+  if (accum && !split && !fixed) {  // continue from the stored rows
     const float* src = out + (size_t)t.row0 * D;
-    for (int i = threadIdx.x; i < n; i += NT) {
+    for (int i = threadIdx.x; i < n; i += kFwdThreads) {
       const int r = i / D;
-      acc[r * DS + (i - r * D)] = T(src[i]);
+      acc[r * DS + (i - r * D)] = src[i];
     }
   } else {
-    for (int i = threadIdx.x; i < nrows * DS; i += NT) acc[i] = T(0);
+    for (int i = threadIdx.x; i < nrows * DS; i += kFwdThreads) acc[i] = 0.0;
   }
   __syncthreads();
 
-  // lanes per edge: VEC==4 => k % 4 == 0 and k/4 <= 64; VEC==1 => min(k, 64) lanes that
-  // loop over the row's k entries.
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
   const int L = (VEC == 4) ? (C3 ? (k + 2) / 3 : k / 4) : (k < kWave ? k : kWave);
   const int EPS = kWave / L;  // edges per wave instruction
@@ -547,41 +472,33 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   const int slot = lane / L;
   const int l0 = (lane - slot * L) * (C3 ? 1 : VEC);
   const bool lane_on = slot < EPS;
-  constexpr int kWaves = NT / kWave;
+  constexpr int kWaves = kFwdThreads / kWave;
 
   if constexpr (VEC == 4) {
-    // U sub-steps per iteration with every load issued before the first LDS update: the
-    // chain (col, val) -> CBSR record -> LDS has two dependent global round trips, so
-    // memory-level parallelism comes from U independent sub-steps per wave. Out-of-range
-    // lanes load a clamped (valid) edge and skip the update.
     auto sweep = [&](auto* a, auto tag) {
       using AA = decltype(tag);
       if (emid >= 0) {
-        fwd_edges4<U, AA, FL>(a, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                              rec_bytes, seltab, DS, k, fsc);
-        fwd_edges4<U, AA, FL>(a, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                              rec_bytes, seltab, DS, k, fsc);
+        fwd_edges4<AA, FL>(a, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+                           rec_bytes, seltab, ss, DS, k, fsc);
+        fwd_edges4<AA, FL>(a, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+                           rec_bytes, seltab, ss, DS, k, fsc);
       } else {
-        fwd_edges4<U, AA, FL>(a, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
-                              rec_bytes, seltab, DS, k, fsc);
+        fwd_edges4<AA, FL>(a, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+                           rec_bytes, seltab, ss, DS, k, fsc);
       }
     };
-    if constexpr (ACC == MAXK_ACC_F64) {
-      if (fixed) sweep(acc64, LdsFix{});
-      else sweep(acc, A{});
-    } else {
-      sweep(acc, A{});
-    }
+    if (fixed) sweep(acc64, LdsFix{});
+    else sweep(acc, LdsF64{});
   } else {
     for (int base = t.e0 + wave * EPS; base < t.e1; base += kWaves * EPS) {
       const int e = base + slot;
       if (lane_on && e < t.e1) {
         const uint2 w = cv[e];
-        const uint32_t cwv = w.x;
         const float v = __uint_as_float(w.y);
-        T* arow = acc + (cwv >> kFwdColBits) * DS;
-        const size_t rb = (size_t)(cwv & kFwdColMask) * k;
-        for (int l = l0; l < k; l += L) A::add(arow + sp_index[rb + l], v * sp_data[rb + l]);
+        double* arow = acc + (w.x >> kFwdColBits) * DS;
+        const size_t c = w.x & kFwdColMask;
+        for (int l = l0; l < k; l += L)
+          LdsF64::add2(arow + sp_index[c * ss + l], v, sp_data[c * ds + l]);
       }
     }
   }
@@ -595,9 +512,9 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     return (float)acc[r * DS + (i - r * D)];
   };
   if (!split) {
-    const bool add = cont && fixed;  // the prior row is added here (see above)
+    const bool add = accum && fixed;  // the prior row is added here (see above)
     if ((D & 3) == 0) {
-      for (int i = threadIdx.x * 4; i < n; i += NT * 4) {
+      for (int i = threadIdx.x * 4; i < n; i += kFwdThreads * 4) {
         float4 v = make_float4(get(i), get(i + 1), get(i + 2), get(i + 3));
         if (add) {
           const float4 o = *reinterpret_cast<const float4*>(dst + i);
@@ -606,12 +523,11 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
         *reinterpret_cast<float4*>(dst + i) = v;
       }
     } else {
-      for (int i = threadIdx.x; i < n; i += NT) dst[i] = add ? dst[i] + get(i) : get(i);
+      for (int i = threadIdx.x; i < n; i += kFwdThreads) dst[i] = add ? dst[i] + get(i) : get(i);
     }
   } else {
-    for (int i = threadIdx.x; i < D; i += NT) global_add(dst + i, get(i));
+    for (int i = threadIdx.x; i < D; i += kFwdThreads) global_add(dst + i, get(i));
   }
-  }  // task loop
 }
 
 __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, float* out,
@@ -623,203 +539,70 @@ __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, fl
 }
 
 // --------------------------------------------------------------------------------------
-// backward
+// backward: column blocks
 // --------------------------------------------------------------------------------------
-// Flat edge processing in (column block, destination row) order: the edges one wave
-// instruction covers share few rows of grad_out, so its gathers stay in the CU's L1. Any
-// wave may update any column of the block (that is what keeps the row locality), hence the
-// atomic LDS accumulation.
-template <int F, int ACC, int U>
-__global__ __launch_bounds__(kBwdThreads) void sspmm_bwd_kernel(
-    const BwdTask* __restrict__ tasks, const int32_t* __restrict__ erow,
-    const int32_t* __restrict__ ecol, const float* __restrict__ evals,
-    const float* __restrict__ G, const uint8_t* __restrict__ sp_index,
-    float* __restrict__ grad_sp, int D, int k) {
-  using A = LdsAcc<ACC>;
-  using T = typename A::T;
-  extern __shared__ __align__(16) double bsmem[];
-  // Accumulator of column c, slot l at c * KS + l with KS = k + 1 (odd, so different columns
-  // start on different banks); the lanes of one edge update consecutive slots (the plain
-  // [c][k] layout with lane-contiguous slots put a wave on 8 banks: 8-way conflicts).
-  T* bacc = reinterpret_cast<T*>(bsmem);
-  const BwdTask t = tasks[blockIdx.x];
-  if (t.ncols == 0 || (t.shared && t.e0 == t.e1)) return;  // padding / nothing to add
-  const int KS = k + 1;
-  const int nacc = t.ncols * KS;
-  for (int i = threadIdx.x; i < nacc; i += kBwdThreads) bacc[i] = T(0);
-  __syncthreads();
-
-  const int L = (F == 4) ? k / 4 : (k < kWave ? k : kWave);  // lanes per edge
-  const int EPS = kWave / L;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
-  const int slot = lane / L;
-  const int q = lane - slot * L;
-  const bool lane_on = slot < EPS;
-  constexpr int kWaves = kBwdThreads / kWave;
-  const int last = t.e1 - 1;
-
-  for (int base = t.e0 + wave * EPS * U; base < t.e1; base += kWaves * EPS * U) {
-    int r[U], c[U];
-    float v[U];
-    bool ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = base + u * EPS + slot;
-      ok[u] = lane_on && e < t.e1;
-      const int ec = ok[u] ? e : last;
-      r[u] = erow[ec];
-      c[u] = ecol[ec];
-      v[u] = evals[ec];
-    }
-    if constexpr (F == 4) {
-      // Lane q of an edge owns the selector slots q, q + L, q + 2L, q + 3L: in gather
-      // instruction i the L lanes of the edge read L adjacent (sorted) selectors of the
-      // row, i.e. ~1-2 cache lines of grad_out[r] instead of L lines. The selector words
-      // are loaded as dwords (lane q: slots 4q..4q+3) and redistributed with shuffles.
-      uint32_t sel[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t w = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)c[u] * k + q * 4);
-        uint32_t m = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int l = q + L * i;  // slot owned by this lane in gather i
-          const uint32_t wi = (uint32_t)__shfl((int)w, slot * L + (l >> 2), kWave);
-          m |= ((wi >> ((l & 3) * 8)) & 0xffu) << (8 * i);
-        }
-        sel[u] = m;
-      }
-      float g[U][4];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float* grow = G + (size_t)r[u] * D;
-        g[u][0] = grow[sel[u] & 0xffu];
-        g[u][1] = grow[(sel[u] >> 8) & 0xffu];
-        g[u][2] = grow[(sel[u] >> 16) & 0xffu];
-        g[u][3] = grow[sel[u] >> 24];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (ok[u]) {
-          T* a = bacc + (c[u] - t.col0) * KS + q;
-          A::add(a, v[u] * g[u][0]);
-          A::add(a + L, v[u] * g[u][1]);
-          A::add(a + 2 * L, v[u] * g[u][2]);
-          A::add(a + 3 * L, v[u] * g[u][3]);
-        }
-      }
-    } else if (k <= kWave) {
-      // one feature per lane: the L = k lanes of an edge read k dwords of the same
-      // grad_out row in one instruction (~7 cache lines at k = 16 instead of 16 for 4
-      // features per lane over 4 instructions); the gather is bound by lines per request.
-      uint32_t sel[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) sel[u] = sp_index[(size_t)c[u] * k + q];
-      float g[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) g[u] = G[(size_t)r[u] * D + sel[u]];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (ok[u]) A::add(bacc + (c[u] - t.col0) * KS + q, v[u] * g[u]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (ok[u]) {
-          const float* grow = G + (size_t)r[u] * D;
-          const uint8_t* srow = sp_index + (size_t)c[u] * k;
-          T* a = bacc + (c[u] - t.col0) * KS;
-          for (int l = q; l < k; l += L) A::add(a + l, v[u] * grow[srow[l]]);
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  float* dst = grad_sp + (size_t)t.col0 * k;
-  const int n = t.ncols * k;
-  for (int i = threadIdx.x; i < n; i += kBwdThreads) {
-    const int cl = i / k;
-    const int l = i - cl * k;
-    const int pos = cl * KS + l;
-    if (t.shared) global_add(dst + i, (float)bacc[pos]);
-    else dst[i] = (float)bacc[pos];
-  }
-}
-
-
-// Packed backward (k % 4 == 0, f32 accumulators): the same (block, row)-ordered sweep as
-// sspmm_bwd_kernel<4, ...> with the per-edge work cut to the memory operations it needs:
-// one dwordx3 record load {row * D * 4, column in block, val}, one dword of four selectors
-// already in lane order (pack_sel_kernel), four buffer_load_dword gathers of grad_out with
-// 32-bit offsets, and the LDS compare-and-swap adds issued as a batch (all reads, then all
-// CAS, then a retry loop for the rare lanes whose CAS lost a race).
-__global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int n, int k, int S,
-                                uint32_t* __restrict__ sel, const int32_t* __restrict__ corder) {
-  // sel[(g * n + c) * L + q] = slots g*k/S + q + L*i, i = 0..3, of the column at block
-  // position c (corder[c], or c itself) (L = k / 4S)
-  const int L = k / (4 * S);
+// Selector words in lane order (per call): word (g * n + c) * L + q of the F-slot kernel holds
+// the F selectors of lane q of column position c in slot group g, slots g * ns + q + L * i
+// (i = 0 .. F-1, L = ns / F lanes, ns = kp / S slots per group), as F bytes. Slots >= k (the
+// padding up to kp) select feature 0; their accumulators are never stored.
+template <int F>
+__global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int is, int n, int k,
+                                int kp, int S,
+                                std::conditional_t<F == 4, uint32_t, uint16_t>* __restrict__ sel,
+                                const int32_t* __restrict__ corder) {
+  const int ns = kp / S;
+  const int L = ns / F;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * L * S) return;
   const int g = i / (n * L);
   const int r = i - g * (n * L);
   const int c = r / L, q = r - c * L;
-  const uint8_t* s = sp_index + (size_t)(corder ? corder[c] : c) * k + g * (k / S) + q;
-  sel[i] = (uint32_t)s[0] | ((uint32_t)s[L] << 8) | ((uint32_t)s[2 * L] << 16) |
-           ((uint32_t)s[3 * L] << 24);
+  const uint8_t* s = sp_index + (size_t)(corder ? corder[c] : c) * is;
+  uint32_t w = 0u;
+#pragma unroll
+  for (int j = 0; j < F; ++j) {
+    const int l = g * ns + q + L * j;
+    w |= (uint32_t)(l < k ? s[l] : 0u) << (8 * j);
+  }
+  sel[i] = (std::conditional_t<F == 4, uint32_t, uint16_t>)w;
 }
 
-// Two slots per lane (sspmm_bwd4_kernel<.., F = 2>): sel[(g * n + c) * L + q] = slots
-// g*k/S + q and g*k/S + q + L of column c (L = k / 2S), as one u16.
-__global__ void pack_sel2_kernel(const uint8_t* __restrict__ sp_index, int n, int k, int S,
-                                 uint16_t* __restrict__ sel, const int32_t* __restrict__ corder) {
-  const int L = k / (2 * S);
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n * L * S) return;
-  const int g = i / (n * L);
-  const int r = i - g * (n * L);
-  const int c = r / L, q = r - c * L;
-  const uint8_t* s = sp_index + (size_t)(corder ? corder[c] : c) * k + g * (k / S) + q;
-  sel[i] = (uint16_t)(s[0] | (s[L] << 8));
-}
-
-// NT threads per work-group (8, 12 or 16 waves: more waves, more gathers in flight per CU
-// under the same LDS block). PF: the next sub-steps' records are loaded right after this
-// step's gathers are issued, so the record stream's HBM latency overlaps the LDS updates
-// (loads retire in issue order, so they must not precede the gathers the updates wait on).
-//
-// V (plan->bwd_cas64): lane q's F slots are stored adjacently (slot l of a column at
-// (l % L) * F + l / L), so its updates are 1 ds_read_b128 + 2 ds_cmpst_rtn_b64 (F = 4) or
-// 1 ds_read_b64 + 1 ds_cmpst_rtn_b64 (F = 2) instead of F + F dword operations (KS % F == 0);
-// a pair is retried if either of its floats changed.
-//
-// F: selector slots per lane, L = k / (F S) lanes per edge. F = 4: a gather instruction
-// covers slots 4i..4i+3 (a quarter of the sorted selectors) of 64/L edges; F = 2: slots
-// 8i..8i+7 of half as many edges, so of about half as many rows of G.
-template <int U, int NT, bool PF, bool V, bool Q, int F = 4>
+// One work-group per (column block, row chunk piece, slot group) task, NT threads (8 waves,
+// 12 at k >= 32: more gathers in flight per CU under the same LDS block). Lanes: L = ns / F
+// per edge, lane q owns the F slots q, q + L, ... of its group, stored adjacently in LDS
+// (slot l of a column at (l % L) * F + l / L), so an update is 1 ds_read_b128 + 2
+// ds_cmpst_rtn_b64 (F = 4) or 1 ds_read_b64 + 1 ds_cmpst_rtn_b64 (F = 2); a pair is retried
+// if either of its floats changed. The block's selector words are staged in LDS behind the
+// accumulators (the G rows evict the block's 16 B/column table from the 32 KB L1).
+// Per sub-step a lane loads its edge's record {row offset, column in block, val} (Q: lane q
+// of a quad loads sub-step 4j + q's whole record, DPP hands it on: one record instruction
+// per four sub-steps), reads its selector word from LDS and gathers F floats of the edge's
+// grad_out row with buffer loads (32-bit offsets; BIG: grad_out > 4 GiB, the record holds the
+// row index and the gathers are 64-bit addressed). Records past e1 (padding or a
+// neighbouring task's) are loaded and ignored.
+template <int U, int NT, int F, bool Q, bool BIG>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
-    const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
-    float* __restrict__ grad_sp, int k, int S, int ncols_all, int KS, int sel_lds,
-    float* __restrict__ slab, const int32_t* __restrict__ corder) {
+    const float* __restrict__ G, uint32_t g_bytes, int D,
+    const std::conditional_t<F == 4, uint32_t, uint16_t>* __restrict__ sel,
+    float* __restrict__ grad_sp, int k, int ns, int ncols_all, float* __restrict__ slab,
+    const int32_t* __restrict__ corder) {
+  static_assert(F == 2 || F == 4, "2 or 4 slots per lane");
+  static_assert(!Q || U % 4 == 0, "quad record loads need U % 4 == 0");
+  using SelT = std::conditional_t<F == 4, uint32_t, uint16_t>;
+  using u64 = unsigned long long;
   extern __shared__ __align__(16) double bsmem[];
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
-  // padding / nothing to add (with the slab flush every chunk stores its block, zeros too)
+  // padding / nothing to add (with the slab flush every piece stores its block, zeros too)
   if (t.ncols == 0 || (t.shared && !slab && t.e0 == t.e1)) return;
-  static_assert(F == 2 || F == 4, "2 or 4 slots per lane");
-  using SelT = std::conditional_t<F == 4, uint32_t, uint16_t>;  // the F selectors of a lane
-  const int ns = k / S;  // slots of this group: [t.group * ns, (t.group + 1) * ns)
-  const int L = ns / F;  // lanes per edge, F slots each: q, q + L, ...
+  const int L = ns / F;   // lanes per edge
+  const int KS = ns;      // accumulator floats per column
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
-  // sel_lds: the block's selector words are staged in LDS behind the accumulator, so the
-  // per-edge selector lookup is an LDS read instead of an L1 miss (the G rows evict the
-  // block's 16 B/column table from the 32 KB L1)
-  const SelT* selg = reinterpret_cast<const SelT*>(sel) + ((size_t)t.group * ncols_all + t.col0) * L;
+  const SelT* selg = sel + ((size_t)t.group * ncols_all + t.col0) * L;
   SelT* sell = reinterpret_cast<SelT*>(bacc + ((nacc + 3) & ~3));
-  if (sel_lds)
-    for (int i = threadIdx.x; i < t.ncols * L; i += NT) sell[i] = selg[i];
+  for (int i = threadIdx.x; i < t.ncols * L; i += NT) sell[i] = selg[i];
   __syncthreads();
 
   const int EPS = kWave / L;
@@ -832,78 +615,35 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const int stride = kWaves * EPS * U;
   const __amdgpu_buffer_rsrc_t gr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
-  const SelT* selb = (sel_lds ? sell : selg) + q;
-  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + (V ? F * q : q);
+  const SelT* selb = sell + q;
+  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + F * q;
   const uint3* rec3 = reinterpret_cast<const uint3*>(rec);
-
-  // records past e1 (a padded or neighbouring record) are loaded and ignored
-  int base = t.e0 + wave * EPS * U;
-  // Q: lane loads dword min(q & 3, 2) of its edge's record (quad_bcast below)
-  const uint32_t* recw = rec + min(lane & 3, 2);
-  auto load_rec = [&](int e) -> uint3 {
-    if constexpr (Q) return make_uint3(recw[3 * (size_t)e], 0u, 0u);
-    else return rec3[e];
-  };
-  constexpr bool EM = Q && (U % 4) == 0;
   const int qq = lane & 3;
-  // EM: lane q of a quad loads sub-step 4j + q's whole record (records past e1 exist: padding)
-  auto load_rq = [&](int b, uint3 (&rq)[U / 4 > 0 ? U / 4 : 1]) {
-#pragma unroll
-    for (int j = 0; j < U / 4; ++j) rq[j] = rec3[b + (4 * j + qq) * EPS + slot];
-  };
-  uint3 rn[U];
-  uint3 rqn[U / 4 > 0 ? U / 4 : 1];
-  if (PF) {
-    if constexpr (EM) {
-      load_rq(base, rqn);
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + u * EPS + slot, t.e1 - 1));
-    }
-  }
-  // Batched records (quad loads without prefetch, U % 4 == 0): lane q of a quad loads the
-  // whole record of its slot's edge in sub-step 4j + q (the wave's 64 loads cover 4 sub-steps'
-  // 64 consecutive records) and DPP hands each sub-step's record to the quad: one record
-  // instruction per four sub-steps. The sub-steps keep their consecutive edges (edges of a
-  // gather instruction share grad_out rows).
-  for (; base < t.e1; base += stride) {
+
+  for (int base = t.e0 + wave * EPS * U; base < t.e1; base += stride) {
     uint32_t go[U], cl[U];
     float v[U];
     bool ok[U];
-    if constexpr (EM) {
-      uint3 rq[U / 4 > 0 ? U / 4 : 1];
-      if (PF) {
+    if constexpr (Q) {
+      uint3 rq[U / 4];
 #pragma unroll
-        for (int j = 0; j < U / 4; ++j) rq[j] = rqn[j];
-      } else {
-        load_rq(base, rq);
-      }
+      for (int j = 0; j < U / 4; ++j) rq[j] = rec3[base + (4 * j + qq) * EPS + slot];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         ok[u] = lane_on && base + u * EPS + slot < t.e1;
-        const uint3 r3 = rq[u / 4];
-        switch (u & 3) {
-          case 0: go[u] = quad_bcast<0>(r3.x); cl[u] = quad_bcast<0>(r3.y); v[u] = __uint_as_float(quad_bcast<0>(r3.z)); break;
-          case 1: go[u] = quad_bcast<1>(r3.x); cl[u] = quad_bcast<1>(r3.y); v[u] = __uint_as_float(quad_bcast<1>(r3.z)); break;
-          case 2: go[u] = quad_bcast<2>(r3.x); cl[u] = quad_bcast<2>(r3.y); v[u] = __uint_as_float(quad_bcast<2>(r3.z)); break;
-          default: go[u] = quad_bcast<3>(r3.x); cl[u] = quad_bcast<3>(r3.y); v[u] = __uint_as_float(quad_bcast<3>(r3.z)); break;
-        }
+        go[u] = quad_pick(rq[u / 4].x, u);
+        cl[u] = quad_pick(rq[u / 4].y, u);
+        v[u] = __uint_as_float(quad_pick(rq[u / 4].z, u));
       }
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = base + u * EPS + slot;
         ok[u] = lane_on && e < t.e1;
-        const uint3 r3 = PF ? rn[u] : load_rec(e);
-        if constexpr (Q) {
-          go[u] = quad_bcast<0>(r3.x);
-          cl[u] = quad_bcast<1>(r3.x);
-          v[u] = __uint_as_float(quad_bcast<2>(r3.x));
-        } else {
-          go[u] = r3.x;
-          cl[u] = r3.y;
-          v[u] = __uint_as_float(r3.z);
-        }
+        const uint3 r3 = rec3[e];
+        go[u] = r3.x;
+        cl[u] = r3.y;
+        v[u] = __uint_as_float(r3.z);
       }
     }
     uint32_t s[U];
@@ -914,119 +654,68 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int i = 0; i < F; ++i) {
-        const uint32_t off = go[u] + (((s[u] >> (8 * i)) & 0xffu) << 2);
-        x[u][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
+        const uint32_t f = (s[u] >> (8 * i)) & 0xffu;
+        if constexpr (BIG) {
+          x[u][i] = G[(size_t)go[u] * D + f];
+        } else {
+          x[u][i] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(gr, go[u] + (f << 2), 0, 0));
+        }
       }
-    }
-    if (PF) {  // unconditional (clamped): a branch here would make the updates below wait
-               // for these loads too (vmcnt counts both paths)
-      __builtin_amdgcn_sched_barrier(0);  // keep every gather ahead of these loads
-      if constexpr (EM) {
-        load_rq(base + stride, rqn);
-      } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u) rn[u] = load_rec(min(base + stride + u * EPS + slot, t.e1 - 1));
-      }
-      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int i = 0; i < F; ++i) x[u][i] *= v[u];
-    if constexpr (V) {
-      using u64 = unsigned long long;
-      u64 old2[U][F / 2];
+    // all reads, then all CAS, then a retry loop for the rare lanes whose CAS lost a race
+    u64 old2[U][F / 2];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        // one ds_read_b128 / b64 (KS % F == 0); a stale value only costs a CAS retry
-        if constexpr (F == 4) {
-          const uint4 o4 = *reinterpret_cast<const uint4*>(accq + cl[u] * KS);
-          old2[u][0] = (u64)o4.x | ((u64)o4.y << 32);
-          old2[u][1] = (u64)o4.z | ((u64)o4.w << 32);
-        } else {
-          const uint2 o2 = *reinterpret_cast<const uint2*>(accq + cl[u] * KS);
-          old2[u][0] = (u64)o2.x | ((u64)o2.y << 32);
+    for (int u = 0; u < U; ++u) {
+      // one ds_read_b128 / b64 (KS % F == 0); a stale value only costs a CAS retry
+      if constexpr (F == 4) {
+        const uint4 o4 = *reinterpret_cast<const uint4*>(accq + cl[u] * KS);
+        old2[u][0] = (u64)o4.x | ((u64)o4.y << 32);
+        old2[u][1] = (u64)o4.z | ((u64)o4.w << 32);
+      } else {
+        const uint2 o2 = *reinterpret_cast<const uint2*>(accq + cl[u] * KS);
+        old2[u][0] = (u64)o2.x | ((u64)o2.y << 32);
+      }
+    }
+    auto addp = [](u64 o, float a0, float a1) -> u64 {
+      const float lo = __uint_as_float((unsigned)o) + a0;
+      const float hi = __uint_as_float((unsigned)(o >> 32)) + a1;
+      return (u64)__float_as_uint(lo) | ((u64)__float_as_uint(hi) << 32);
+    };
+    u64 got2[U][F / 2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
+#pragma unroll
+      for (int h = 0; h < F / 2; ++h) {
+        got2[u][h] = old2[u][h];
+        if (ok[u]) {
+          u64 expected = old2[u][h];
+          __hip_atomic_compare_exchange_strong(a + h, &expected,
+                                               addp(old2[u][h], x[u][2 * h], x[u][2 * h + 1]),
+                                               __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          got2[u][h] = expected;
         }
       }
-      auto addp = [](u64 o, float a0, float a1) -> u64 {
-        const float lo = __uint_as_float((unsigned)o) + a0;
-        const float hi = __uint_as_float((unsigned)(o >> 32)) + a1;
-        return (u64)__float_as_uint(lo) | ((u64)__float_as_uint(hi) << 32);
-      };
-      u64 got2[U][F / 2];
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
+    for (int u = 0; u < U; ++u) {
+      u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
 #pragma unroll
-        for (int h = 0; h < F / 2; ++h) {
-          got2[u][h] = old2[u][h];
-          if (ok[u]) {
-            u64 expected = old2[u][h];
+      for (int h = 0; h < F / 2; ++h) {
+        if (ok[u] && got2[u][h] != old2[u][h]) {
+          u64 cur = got2[u][h];
+          while (true) {
+            u64 expected = cur;
             __hip_atomic_compare_exchange_strong(a + h, &expected,
-                                                 addp(old2[u][h], x[u][2 * h], x[u][2 * h + 1]),
+                                                 addp(cur, x[u][2 * h], x[u][2 * h + 1]),
                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-            got2[u][h] = expected;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
-#pragma unroll
-        for (int h = 0; h < F / 2; ++h) {
-          if (ok[u] && got2[u][h] != old2[u][h]) {
-            u64 cur = got2[u][h];
-            while (true) {
-              u64 expected = cur;
-              __hip_atomic_compare_exchange_strong(a + h, &expected,
-                                                   addp(cur, x[u][2 * h], x[u][2 * h + 1]),
-                                                   __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-              if (expected == cur) break;
-              cur = expected;
-            }
-          }
-        }
-      }
-      continue;
-    }
-    unsigned old[U][F];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      unsigned* a = accq + cl[u] * KS;
-#pragma unroll
-      for (int i = 0; i < F; ++i)
-        old[u][i] = __hip_atomic_load(a + i * L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    unsigned got[U][F];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      unsigned* a = accq + cl[u] * KS;
-#pragma unroll
-      for (int i = 0; i < F; ++i) {
-        got[u][i] = old[u][i];
-        if (ok[u]) {
-          unsigned expected = old[u][i];
-          __hip_atomic_compare_exchange_strong(
-              a + i * L, &expected, __float_as_uint(__uint_as_float(old[u][i]) + x[u][i]),
-              __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          got[u][i] = expected;
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      unsigned* a = accq + cl[u] * KS;
-#pragma unroll
-      for (int i = 0; i < F; ++i) {
-        if (ok[u] && got[u][i] != old[u][i]) {
-          unsigned cur = got[u][i];
-          while (true) {
-            unsigned expected = cur;
-            __hip_atomic_compare_exchange_strong(
-                a + i * L, &expected, __float_as_uint(__uint_as_float(cur) + x[u][i]),
-                __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (expected == cur) break;
             cur = expected;
           }
@@ -1036,139 +725,23 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   }
   __syncthreads();
 
-  // shared block: global atomics into a zeroed grad_sp, or (slab flush) piece 0 stores into
-  // grad_sp and piece p > 0 into its slab region (block positions), summed by
-  // bwd_combine_kernel; corder maps block positions to the columns of grad_sp
+  // store: piece 0 of a block (or an unsplit block) into grad_sp, piece p > 0 into its slab
+  // region (block positions, summed by bwd_combine_kernel), or (no slabs) global atomics into
+  // a zeroed grad_sp; corder maps block positions to the columns of grad_sp. Padding slots
+  // (>= k) are dropped.
   const bool atomic = t.shared && !slab;
   const bool to_slab = slab && t.slab >= 0;
-  float* dst = to_slab ? slab + t.slab + t.group * ns : grad_sp + t.group * ns;
+  float* dst = to_slab ? slab + t.slab : grad_sp;
+  const int g0 = t.group * ns;
   const int n = t.ncols * ns;
   for (int i = threadIdx.x; i < n; i += NT) {
     const int c = i / ns;
     const int l = i - c * ns;
-    const float a = bacc[c * KS + (V ? (l % L) * F + l / L : l)];
+    if (g0 + l >= k) continue;
+    const float a = bacc[c * KS + (l % L) * F + l / L];
     const size_t row = to_slab ? (size_t)c : (size_t)(corder ? corder[t.col0 + c] : t.col0 + c);
-    if (atomic) global_add(dst + row * k + l, a);
-    else dst[row * k + l] = a;
-  }
-}
-
-// Packed backward with one selector slot per lane (plan->bwd_feats == 1, k <= 64): the k
-// lanes of an edge gather k dwords of ONE row of grad_out in one instruction, so a wave
-// instruction covers 64/k edges that are mostly of the same row (edges are row-sorted in a
-// block) and touches ~8 lines of G, where the 4-slots-per-lane kernel's instructions cover
-// slot group i of 64/(k/4) edges of ~k/4 rows. The gathers are bound by distinct lines per
-// instruction at the L1 (tools/ubench_tcp.hip), not by lanes. The block's selector bytes are
-// staged in LDS straight from sp_index (no per-call packing).
-template <int U, int NT>
-__global__ __launch_bounds__(NT) void sspmm_bwd1_kernel(
-    const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
-    const float* __restrict__ G, uint32_t g_bytes, const uint8_t* __restrict__ sp_index,
-    float* __restrict__ grad_sp, int k, int KS, float* __restrict__ slab,
-    const int32_t* __restrict__ corder) {
-  extern __shared__ __align__(16) double bsmem[];
-  float* bacc = reinterpret_cast<float*>(bsmem);
-  const BwdTask t = tasks[blockIdx.x];
-  // padding / nothing to add (with the slab flush every chunk stores its block, zeros too)
-  if (t.ncols == 0 || (t.shared && !slab && t.e0 == t.e1)) return;
-  const int nacc = t.ncols * KS;
-  for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
-  uint8_t* sell = reinterpret_cast<uint8_t*>(bacc + ((nacc + 3) & ~3));
-  // the block's selector rows: columns corder[col0 ..] (or col0 .. contiguous)
-  auto col_of = [&](int c) -> size_t { return corder ? (size_t)corder[t.col0 + c] : (size_t)t.col0 + c; };
-  const int nsel = t.ncols * k;
-  if ((k & 3) == 0) {
-    const int kw = k / 4;
-    for (int i = threadIdx.x; i < nsel / 4; i += NT) {
-      const int c = i / kw;
-      reinterpret_cast<uint32_t*>(sell)[i] =
-          reinterpret_cast<const uint32_t*>(sp_index + col_of(c) * k)[i - c * kw];
-    }
-  } else {
-    for (int i = threadIdx.x; i < nsel; i += NT) {
-      const int c = i / k;
-      sell[i] = sp_index[col_of(c) * k + (i - c * k)];
-    }
-  }
-  __syncthreads();
-
-  const int L = k;  // lanes per edge
-  const int EPS = kWave / L;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
-  const int slot = lane / L;
-  const int q = lane - slot * L;
-  const bool lane_on = slot < EPS;
-  constexpr int kWaves = NT / kWave;
-  const int stride = kWaves * EPS * U;
-  const __amdgpu_buffer_rsrc_t gr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
-  const uint3* rec3 = reinterpret_cast<const uint3*>(rec);
-  const uint8_t* selq = sell + q;
-  unsigned* accq = reinterpret_cast<unsigned*>(bacc) + q;
-
-  for (int base = t.e0 + wave * EPS * U; base < t.e1; base += stride) {
-    uint32_t go[U], cl[U];
-    float v[U];
-    bool ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = base + u * EPS + slot;  // past e1: a padded or neighbouring record
-      ok[u] = lane_on && e < t.e1;
-      const uint3 r3 = rec3[e];
-      go[u] = r3.x;
-      cl[u] = r3.y;
-      v[u] = __uint_as_float(r3.z);
-    }
-    float x[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t off = go[u] + ((uint32_t)selq[cl[u] * k] << 2);
-      x[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) x[u] *= v[u];
-    unsigned old[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      old[u] = __hip_atomic_load(accq + cl[u] * KS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    unsigned got[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      got[u] = old[u];
-      if (ok[u]) {
-        unsigned expected = old[u];
-        __hip_atomic_compare_exchange_strong(
-            accq + cl[u] * KS, &expected, __float_as_uint(__uint_as_float(old[u]) + x[u]),
-            __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        got[u] = expected;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (ok[u] && got[u] != old[u]) {
-        unsigned cur = got[u];
-        while (true) {
-          unsigned expected = cur;
-          __hip_atomic_compare_exchange_strong(
-              accq + cl[u] * KS, &expected, __float_as_uint(__uint_as_float(cur) + x[u]),
-              __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (expected == cur) break;
-          cur = expected;
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  const bool atomic = t.shared && !slab;
-  const bool to_slab = slab && t.slab >= 0;
-  for (int i = threadIdx.x; i < nsel; i += NT) {
-    const int c = i / k;
-    const float a = bacc[c * KS + (i - c * k)];
-    float* dst = to_slab ? slab + t.slab + i : grad_sp + col_of(c) * k + (i - c * k);
-    if (atomic) global_add(dst, a);
-    else *dst = a;
+    if (atomic) global_add(dst + row * k + g0 + l, a);
+    else dst[row * k + g0 + l] = a;
   }
 }
 
@@ -1216,95 +789,24 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(float* __restrict__ gr
   }
 }
 
-// Column-major backward for sparse graphs (plan->bwd_csc): the records are sorted by column
-// (stable, so rows ascend within a column) and one wavefront owns a column c. Its L = k/F
-// lanes per edge (F = 4: interleaved slots q + L*i from the packed selector word; F = 1: one
-// slot per lane straight from sp_index) load the column's selectors once, then the wave
-// walks the column's edges 64/L at a time, gathering k features of each source row of
-// grad_out and summing them in registers; a shuffle-xor reduction over the edge slots leaves
-// the k sums in lanes 0..L-1, which store them. No LDS, no atomics, no memset: every column
-// is written exactly once.
-template <int F, int U>
-__global__ __launch_bounds__(256) void sspmm_bwd_csc_kernel(
-    const int32_t* __restrict__ colptr, const uint32_t* __restrict__ rec,
-    const float* __restrict__ G, uint32_t g_bytes, const uint32_t* __restrict__ sel,
-    const uint8_t* __restrict__ sp_index, float* __restrict__ grad_sp, int ncols, int k) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int c = blockIdx.x * (256 / kWave) + threadIdx.x / kWave;
-  if (c >= ncols) return;
-  const int L = k / F;  // power of two <= 64 (checked by the plan)
-  const int EPS = kWave / L;
-  const int slot = lane / L;
-  const int q = lane - slot * L;
-  uint32_t so[F];
-  if constexpr (F == 4) {
-    const uint32_t s = sel[(size_t)c * L + q];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) so[i] = ((s >> (8 * i)) & 0xffu) << 2;
-  } else {
-    so[0] = (uint32_t)sp_index[(size_t)c * k + q] << 2;
-  }
-  const int e0 = colptr[c], e1 = colptr[c + 1];
-  const __amdgpu_buffer_rsrc_t gr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
-  float acc[F];
-#pragma unroll
-  for (int i = 0; i < F; ++i) acc[i] = 0.f;
-  for (int base = e0; base < e1; base += EPS * U) {
-    uint32_t go[U];
-    float v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = base + u * EPS + slot;
-      if (e < e1) {
-        const uint3 r3 = *reinterpret_cast<const uint3*>(rec + 3 * (size_t)e);
-        go[u] = r3.x;
-        v[u] = __uint_as_float(r3.z);
-      } else {
-        go[u] = 0;
-        v[u] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool ok = base + u * EPS + slot < e1;
-#pragma unroll
-      for (int i = 0; i < F; ++i) {
-        // out-of-range offset for the idle slots: the buffer load returns 0 (no 0 * inf)
-        const uint32_t off = ok ? go[u] + so[i] : 0xfffffffcu;
-        acc[i] = fmaf(v[u], __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gr, off, 0, 0)), acc[i]);
-      }
-    }
-  }
-  for (int m = L; m < kWave; m <<= 1) {
-#pragma unroll
-    for (int i = 0; i < F; ++i) acc[i] += __shfl_xor(acc[i], m, kWave);
-  }
-  if (slot == 0) {
-    float* dst = grad_sp + (size_t)c * k + q;
-#pragma unroll
-    for (int i = 0; i < F; ++i) dst[i * L] = acc[i];
-  }
-}
-
-// Two-pass backward (plan->bwd_twopass), pass 1: one wavefront per R consecutive destination
-// rows stages their grad_out rows in its LDS once, then walks their (contiguous) edges 64/L
-// at a time (L = k/4 lanes per edge): lane q of an edge on column c reads the 4 selectors
-// sp_index[c][4q..4q+3] (one dword), multiplies the 4 staged features of the edge's row
-// (row % R from the edge record) by val and stores them as one float4 into the edge's slot
-// T[e][4q..] (CSR order: the slots of a wavefront are contiguous, the stores coalesce; in
-// column order the scattered 64-B stores ran at a quarter of the bandwidth). The only gathers
-// left on the texture path are the k selector bytes per edge; grad_out is read once.
+// --------------------------------------------------------------------------------------
+// backward: two passes (low row reuse)
+// --------------------------------------------------------------------------------------
+// Pass 1: one wavefront per R consecutive destination rows stages their grad_out rows in its
+// LDS once, then walks their (contiguous) edges 64/L at a time (L = k/4 lanes per edge): lane
+// q of an edge on column c reads the 4 selectors sp_index[c][4q..4q+3] (one dword),
+// multiplies the 4 staged features of the edge's row (row % R from the edge record) by val
+// and stores them as one float4 into the edge's slot T[e][4q..] (CSR order: the slots of a
+// wavefront are contiguous, the stores coalesce; in column order the scattered stores ran
+// 7-18 % slower, profiles/r02/bwd_probe/twopass_store_order.jsonl). The only gathers left on
+// the texture path are the k selector bytes per edge; grad_out is read once.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// CS (plan->bwd_tp_csc): each edge's k products go to its column-order slot pos[e] of the
-// workspace (full 128-B lines at k = 32), so the column pass streams its slots contiguously
-// instead of gathering them through bwd_perm.
-template <int U, int R, bool CS = false>
+template <int U, int R>
 __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
     const int32_t* __restrict__ ptr, const uint32_t* __restrict__ erec,
-    const float* __restrict__ G, const uint8_t* __restrict__ sp_index, float* __restrict__ T,
-    int rbeg, int rend, int64_t ebase, int D, int k, const int32_t* __restrict__ pos) {
+    const float* __restrict__ G, const uint8_t* __restrict__ sp_index, int is,
+    float* __restrict__ T, int rbeg, int rend, int64_t ebase, int D, int k) {
   // R rows of kMaxDim floats per wavefront (any u8 selector stays inside the wave's rows).
   // This launch covers destination rows [rbeg, rend), whose edges [ptr[rbeg], ptr[rend])
   // have their slots at T + (e - ebase) * k (one row chunk of the workspace)
@@ -1358,18 +860,14 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
       const int qq = lane & 3;
 #pragma unroll
       for (int j = 0; j < U / 4; ++j) {
-        const uint2 w = *reinterpret_cast<const uint2*>(
+        const uint2 w2 = *reinterpret_cast<const uint2*>(
             erec + 2 * (size_t)min(base + (4 * j + qq) * EPS + slot, e1 - 1));
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int u = 4 * j + i;
           if (u >= U) break;
-          switch (i) {
-            case 0: c[u] = quad_bcast<0>(w.x); v[u] = __uint_as_float(quad_bcast<0>(w.y)); break;
-            case 1: c[u] = quad_bcast<1>(w.x); v[u] = __uint_as_float(quad_bcast<1>(w.y)); break;
-            case 2: c[u] = quad_bcast<2>(w.x); v[u] = __uint_as_float(quad_bcast<2>(w.y)); break;
-            default: c[u] = quad_bcast<3>(w.x); v[u] = __uint_as_float(quad_bcast<3>(w.y)); break;
-          }
+          c[u] = quad_pick(w2.x, i);
+          v[u] = __uint_as_float(quad_pick(w2.y, i));
         }
       }
     } else {
@@ -1384,27 +882,11 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
     uint32_t sw[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      sw[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)(c[u] & kFwdColMask) * k + 4 * q);
-    int32_t ps[U];
-    if constexpr (CS) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) ps[u] = pos[min(base + u * EPS + slot, e1 - 1)];
-    }
+      sw[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)(c[u] & kFwdColMask) * is + 4 * q);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = base + u * EPS + slot;
       const float* rw = row + (R > 1 ? (c[u] >> kFwdColBits) * kMaxDim : 0);
-      if constexpr (CS) {
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        f4v o;
-        o.x = v[u] * rw[sw[u] & 0xffu];
-        o.y = v[u] * rw[(sw[u] >> 8) & 0xffu];
-        o.z = v[u] * rw[(sw[u] >> 16) & 0xffu];
-        o.w = v[u] * rw[sw[u] >> 24];
-        if (e < e1)
-          __builtin_nontemporal_store(o, reinterpret_cast<f4v*>(T + (size_t)ps[u] * k + 4 * q));
-        continue;
-      }
       const uint32_t off = e < e1 ? ((uint32_t)(e - e0) * (uint32_t)k + 4u * q) * 4u : 0xfffffff0u;
       u32x4 o;
       o.x = __float_as_uint(v[u] * rw[sw[u] & 0xffu]);
@@ -1418,13 +900,13 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
   }
 }
 
-// Two-pass backward, pass 2: one wavefront per column c sums the slots of the column's
-// in-edges perm[lo[c] .. hi[c]) (64/L slots per step, float4 per lane), reduces over the
-// slots with shuffles and stores grad_sp[c] (every column written once: no memset, no
-// atomics). Row chunks (plan->bwd_tp_chunks > 1): this pass covers the in-edges of one row
-// chunk, whose slots are at T + (perm - ebase) * k; chunk 0 stores, later chunks add to the
-// stored sums in chunk order (deterministic).
-template <int U, bool CS = false>
+// Pass 2: one wavefront per column c sums the slots of the column's in-edges perm[lo[c] ..
+// hi[c]) (64/L slots per step, float4 per lane), reduces over the slots with shuffles and
+// stores grad_sp[c] (every column written once: no memset, no atomics). Row chunks
+// (plan->bwd_tp_chunks > 1): this pass covers the in-edges of one row chunk, whose slots are
+// at T + (perm - ebase) * k; chunk 0 stores, later chunks add to the stored sums in chunk
+// order (deterministic).
+template <int U>
 __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
     const int32_t* __restrict__ lo, const int32_t* __restrict__ hi,
     const int32_t* __restrict__ perm, const float* __restrict__ T, int64_t ebase,
@@ -1440,7 +922,7 @@ __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int base = e0; base < e1; base += EPS * U) {
     int32_t pe[U];
-    if (!CS && (U & 3) == 0 && (L & 3) == 0) {
+    if ((U & 3) == 0 && (L & 3) == 0) {
       // lane q of a quad loads the permutation entry of sub-step 4j + q, DPP hands it on
       const int qq = lane & 3;
 #pragma unroll
@@ -1450,20 +932,13 @@ __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
         for (int i = 0; i < 4; ++i) {
           const int u = 4 * jj + i;
           if (u >= U) break;
-          switch (i) {
-            case 0: pe[u] = (int32_t)quad_bcast<0>(w); break;
-            case 1: pe[u] = (int32_t)quad_bcast<1>(w); break;
-            case 2: pe[u] = (int32_t)quad_bcast<2>(w); break;
-            default: pe[u] = (int32_t)quad_bcast<3>(w); break;
-          }
+          pe[u] = (int32_t)quad_pick(w, i);
         }
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = min(base + u * EPS + slot, e1 - 1);
-        pe[u] = CS ? j : (int32_t)(perm[j] - ebase);  // CS: the slots are already in column order
-      }
+      for (int u = 0; u < U; ++u)
+        pe[u] = (int32_t)(perm[min(base + u * EPS + slot, e1 - 1)] - ebase);
     }
     float4 t[U];
 #pragma unroll
@@ -1500,6 +975,9 @@ __global__ __launch_bounds__(256) void sspmm_bwd_cols_kernel(
   }
 }
 
+// --------------------------------------------------------------------------------------
+// dense comparator
+// --------------------------------------------------------------------------------------
 // Dense CSR SpMM (DGL update_all(copy_u, sum) with edge weights: the ReLU layers' dense
 // aggregation and the dense comparator). One wavefront per destination row; the row's
 // D/4 float4 chunks take L lanes (the next power of two, <= 64) and the wave's 64/L edge
@@ -1554,14 +1032,13 @@ __global__ __launch_bounds__(256) void dense_spmm_kernel(
   }
 }
 
-size_t acc_bytes(int acc) { return acc == MAXK_ACC_F32_CAS ? sizeof(float) : sizeof(double); }
-
-size_t fwd_lds_bytes(int tile_rows, int D, int acc) {
-  return (size_t)tile_rows * (D + kFwdRowPad) * acc_bytes(acc);
+size_t fwd_lds_bytes(int tile_rows, int D) {
+  return (size_t)tile_rows * (D + kFwdRowPad) * sizeof(double);
 }
 
-size_t bwd_lds_bytes(int block_cols, int k, int acc) {
-  return (size_t)block_cols * (k + 1) * acc_bytes(acc);
+// LDS of a column-block work-group: C x KS f32 accumulators, then C x ns selector bytes
+size_t bwd_lds_bytes(int block_cols, int ks) {
+  return ((size_t)block_cols * ks + 3) / 4 * 4 * sizeof(float) + (size_t)block_cols * ks;
 }
 
 template <typename K>
@@ -1575,13 +1052,14 @@ static hipError_t allow_lds(K* kernel, size_t bytes) {
 using namespace maxk;
 
 // Fixed-point statistics of a CBSR table into two zeroed words: the lane-parallel kernel
-// for k % 4 == 0 (~10 us for Reddit at k = 16), one thread per row otherwise.
+// for k % 4 == 0 (~10 us for Reddit at k = 16), one thread per row otherwise. Rows of the
+// table are ds floats (values) / is bytes (selectors) apart.
 // rec != nullptr (k % 4 == 0 only): also pack the forward's CBSR records (st0 == nullptr: the
-// pack alone)
-// zrows/nz/out/D (k % 4 == 0 only): split rows of the forward to zero in the same launch.
-static int launch_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int64_t nrows, int k,
-                             uint32_t* st0, uint32_t* st1, int cus, hipStream_t s,
-                             uint8_t* rec = nullptr, int rec_bytes = 0,
+// pack alone); zrows/nz/out/D (k % 4 == 0 only): split rows of the forward to zero in the
+// same launch.
+static int launch_cbsr_stats(const float* sp_data, int ds, const uint8_t* sp_index, int is,
+                             int64_t nrows, int k, uint32_t* st0, uint32_t* st1, int cus,
+                             hipStream_t s, uint8_t* rec = nullptr, int rec_bytes = 0,
                              const int32_t* zrows = nullptr, int nz = 0, float* out = nullptr,
                              int D = 0) {
   if (nrows <= 0) return MAXK_OK;
@@ -1594,17 +1072,17 @@ static int launch_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int6
         1, std::min<int64_t>((nrows + rows_per_block - 1) / rows_per_block, cap));
     if (rec && st0)
       hipLaunchKernelGGL((cbsr_stats4_kernel<true, true>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D);
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D, ds, is);
     else if (rec)
       hipLaunchKernelGGL((cbsr_stats4_kernel<true, false>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D);
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D, ds, is);
     else
       hipLaunchKernelGGL((cbsr_stats4_kernel<false, true>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D);
+                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D, ds, is);
   } else {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nrows + 255) / 256, 2 * cus));
     hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nrows,
-                       k, st0, st1);
+                       k, st0, st1, ds, is);
   }
   MAXK_LAUNCH_CHECK("cbsr_stats launch");
   return MAXK_OK;
@@ -1621,12 +1099,21 @@ static int check_plan(const maxk_plan* plan, const int32_t* ptr, const int32_t* 
   return MAXK_OK;
 }
 
+// Table row strides: 0 means k; values in floats, selectors in bytes.
+static int table_strides(int64_t& ds, int64_t& is, int k, const char* who) {
+  if (ds == 0) ds = k;
+  if (is == 0) is = k;
+  MAXK_CHECK_ARG(ds >= k && is >= k && ds <= INT32_MAX / 4 && is <= INT32_MAX,
+                 std::string(who) + ": table row strides must be >= k (0: k)");
+  return MAXK_OK;
+}
+
 static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const int32_t* idx,
-                               const float* val, const float* sp_data, const uint8_t* sp_index,
-                               float* out, int32_t N, int64_t E, int32_t k, int32_t D,
-                               void* stream, int accum, void* ws, int64_t ws_bytes,
-                               const uint32_t* stats = nullptr, int n_stats = 0,
-                               int64_t stats_stride = 2) {
+                               const float* val, const float* sp_data, int64_t ds64,
+                               const uint8_t* sp_index, int64_t is64, float* out, int32_t N,
+                               int64_t E, int32_t k, int32_t D, void* stream, int accum,
+                               void* ws, int64_t ws_bytes, const uint32_t* stats = nullptr,
+                               int n_stats = 0, int64_t stats_stride = 2) {
   MAXK_CHECK_ARG(N >= 0 && E >= 0, "maxk_spgemm_forward: negative size");
   MAXK_CHECK_ARG(stats == nullptr || (n_stats >= 1 && n_stats <= 1024),
                  "maxk_spgemm_forward_ex: n_stats must be in [1, 1024]");
@@ -1635,13 +1122,15 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
                  "maxk_spgemm_forward_ex: stats_stride must be >= 2 (or 0)");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_spgemm_forward: dim_origin must be in [1, 256]");
   MAXK_CHECK_ARG(k >= 1 && k <= D, "k must be between 1 and input dimension");
+  if (int rc = table_strides(ds64, is64, k, "maxk_spgemm_forward")) return rc;
+  const int ds = (int)ds64, is = (int)is64;
   int rc = check_plan(plan, ptr, idx, N, E, k, D, "maxk_spgemm_forward");
   if (rc) return rc;
   if (N == 0) return MAXK_OK;
   MAXK_CHECK_ARG(out && sp_data && sp_index && (E == 0 || (idx && val)) && ptr,
                  "maxk_spgemm_forward: null pointer");
   (void)val;  // the plan holds the permuted snapshot of (idx, val)
-  uint8_t* ws_base = plan->fwd_rec;  // packed CBSR records (per call)
+  uint8_t* ws_base = plan->fwd_rec;  // packed CBSR records + statistics words (per call)
   if (ws) {
     MAXK_CHECK_ARG(ws_bytes >= plan->fwd_ws_bytes,
                    "maxk_spgemm_forward: workspace smaller than maxk_plan_workspace_bytes");
@@ -1655,15 +1144,17 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   // split rows are summed atomically into zeroed rows: zeroed by the statistics / pack launch
   // when there is one (k % 4 == 0), else by a launch of their own
   const int nz = accum ? 0 : plan->n_zero_rows;
-  const int R = plan->fwd_tile_rows;
-  const int B = plan->fwd_phases;
-  const size_t lds = fwd_lds_bytes(R, D, plan->fwd_acc);
-  const int rec_bytes = plan->fwd_rec_bytes;
-  // two tables: values read straight from sp_data (4k-byte rows), selectors from sp_index
-  const bool two = plan->fwd_two_tables;  // the plan only sets it with k % 4 == 0, no chunks
+  const size_t lds = fwd_lds_bytes(plan->fwd_tile_rows, D);
+  // the caller's tables are already interleaved CBSR records {k values, k selectors} (the
+  // multi-GPU path all-gathers them so): gather from them as they are, no per-call pack
+  const bool inplace = k % 4 == 0 && !plan->fwd_chunk3 &&
+                       sp_index == reinterpret_cast<const uint8_t*>(sp_data) + 4 * (size_t)k &&
+                       is == 4 * ds;
+  // two tables: values read straight from sp_data (ds floats per row), selectors from sp_index
+  const bool two = plan->fwd_two_tables && !inplace;  // the plan only sets it with k % 4 == 0
   const uint8_t* seltab = two ? sp_index : nullptr;
-  const uint8_t* recp = two ? reinterpret_cast<const uint8_t*>(sp_data) : rec_ws;
-  const int rec_bytes_eff = two ? 4 * k : rec_bytes;
+  const uint8_t* recp = (two || inplace) ? reinterpret_cast<const uint8_t*>(sp_data) : rec_ws;
+  const int rec_bytes = (two || inplace) ? 4 * ds : plan->fwd_rec_bytes;
   // fixed-point forward: the call's slot bound / min |x| for fwd_fix_scale (one pass over the
   // CBSR table, fused with the record pack when there is one), or the caller's per-rank pairs
   // (maxk_spgemm_forward_ex)
@@ -1684,12 +1175,12 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       xstat = st;
     }
   }
-  const bool pack4 = !two && !plan->fwd_chunk3 && k % 4 == 0 && plan->num_cols > 0;
+  const bool pack4 = !two && !inplace && !plan->fwd_chunk3 && k % 4 == 0 && plan->num_cols > 0;
   if (plan->fwd_chunk3 && plan->num_cols > 0) {
     const int64_t items = (int64_t)plan->num_cols * ((k + 2) / 3);
     const int grid = (int)std::min<int64_t>((items + 255) / 256, 65536);
     hipLaunchKernelGGL(pack_cbsr3_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
-                       rec_ws, plan->num_cols, k, rec_bytes);
+                       rec_ws, plan->num_cols, k, plan->fwd_rec_bytes, ds, is);
     MAXK_LAUNCH_CHECK("pack_cbsr3 launch");
   }
   const bool zero_in_stats = (pack4 || st) && k % 4 == 0;
@@ -1698,96 +1189,36 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     MAXK_LAUNCH_CHECK("zero_rows launch");
   }
   if (pack4 || st) {
-    const int rc = launch_cbsr_stats(sp_data, sp_index, plan->num_cols, k, st,
-                                     st ? st + 32 : nullptr, plan->cus, s,
-                                     pack4 ? rec_ws : nullptr, rec_bytes, plan->zero_rows,
-                                     zero_in_stats ? nz : 0, out, D);
-    if (rc) return rc;
+    const int rc2 = launch_cbsr_stats(sp_data, ds, sp_index, is, plan->num_cols, k, st,
+                                      st ? st + 32 : nullptr, plan->cus, s,
+                                      pack4 ? rec_ws : nullptr, plan->fwd_rec_bytes,
+                                      plan->zero_rows, zero_in_stats ? nz : 0, out, D);
+    if (rc2) return rc2;
   }
-  const int rot = plan->fwd_rot_ticks;
-  // persistent grid: as many work-groups as fit on the device at once (capped by tasks)
-#define FWD_LAUNCH1(V, A, UU, NT, FL)                                                     \
-  do {                                                                                    \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, A, UU, NT, FL>, lds)); \
-    int per_cu = 0;                                                                       \
-    MAXK_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(                            \
-        &per_cu, spgemm_fwd_kernel<V, A, UU, NT, FL>, NT, lds));                          \
-    const int g = plan->fwd_persistent                                                    \
-                      ? std::max(1, std::min(plan->n_fwd_tasks, std::max(per_cu, 1) * plan->cus)) \
-                      : plan->n_fwd_tasks;                                                \
-    for (int b = 0; b < (rot ? 1 : B); ++b)                                               \
-      hipLaunchKernelGGL((spgemm_fwd_kernel<V, A, UU, NT, FL>), dim3(g), dim3(NT), lds, s, \
-                         plan->fwd_tasks, plan->n_fwd_tasks, plan->fwd_phase_off, B, b,   \
-                         plan->fwd_cv, sp_data, sp_index, recp,                           \
-                         rec_bytes_eff, out, D, k, R, rot, seltab, accum, fix_tab, xstat, \
-                         xs_n, xs_stride, xs_off2);                                       \
-  } while (0)
-#define FWD_LAUNCH(V, A)                                                                  \
-  do {                                                                                    \
-    if (plan->fwd_unroll == 16) FWD_LAUNCH1(V, A, 16, 256, 0);                            \
-    else FWD_LAUNCH1(V, A, 8, 256, 0);                                                    \
-  } while (0)
-#define FWD_LAUNCH_FL(NT)                                                                 \
-  do {                                                                                    \
-    switch (FL & 7) {                                                                     \
-      case 0: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 0); break;                              \
-      case 1: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 1); break;                              \
-      case 2: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 2); break;                              \
-      case 3: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 3); break;                              \
-      case 4: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 4); break;                              \
-      case 5: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 5); break;                              \
-      case 6: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 6); break;                              \
-      default: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, NT, 7); break;                             \
-    }                                                                                     \
-  } while (0)
-#define FWD_LAUNCH_FLQ()                                                                  \
-  do {                                                                                    \
-    switch (FL & 7) {                                                                     \
-      case 0: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 8); break;                             \
-      case 1: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 9); break;                             \
-      case 2: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 10); break;                            \
-      case 3: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 11); break;                            \
-      case 4: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 12); break;                            \
-      case 5: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 13); break;                            \
-      case 6: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 14); break;                            \
-      default: FWD_LAUNCH1(4, MAXK_ACC_F64, 8, 256, 15); break;                           \
-    }                                                                                     \
-  } while (0)
-  const int W = plan->fwd_waves;
+  if (plan->n_fwd_tasks == 0) return MAXK_OK;
   const int Lf = plan->fwd_chunk3 ? (k + 2) / 3 : k / 4;  // lanes per edge
-  const int FL = (plan->fwd_prefetch ? kFwdFlagPrefetch : 0) |
-                 (plan->fwd_branchless ? kFwdFlagBranchless : 0) |
-                 (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0) |
-                 (plan->fwd_quad && Lf % 4 == 0 && W == 4 ? kFwdFlagQuad : 0);
-  if ((k % 4 == 0 || plan->fwd_chunk3) && plan->fwd_acc == MAXK_ACC_F64 &&
-      plan->fwd_unroll == 16 && W == 4) {
-    switch (FL & 7) {  // 16 sub-steps in flight per wave (no quad loads)
-      case 0: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 0); break;
-      case 1: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 1); break;
-      case 2: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 2); break;
-      case 3: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 3); break;
-      case 4: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 4); break;
-      case 5: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 5); break;
-      case 6: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 6); break;
-      default: FWD_LAUNCH1(4, MAXK_ACC_F64, 16, 256, 7); break;
+  const int FL = (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0) |
+                 (plan->fwd_quad && Lf % 4 == 0 ? kFwdFlagQuad : 0);
+#define FWD_LAUNCH(V, FF)                                                                   \
+  do {                                                                                      \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, FF>, lds));             \
+    hipLaunchKernelGGL((spgemm_fwd_kernel<V, FF>), dim3(plan->n_fwd_tasks), dim3(kFwdThreads), \
+                       lds, s, plan->fwd_tasks, plan->fwd_phase_off, plan->fwd_phases,      \
+                       plan->fwd_cv, sp_data, sp_index, recp, rec_bytes, out, D, k,         \
+                       plan->fwd_rot_ticks, seltab, is, ds, accum, fix_tab, xstat, xs_n,     \
+                       xs_stride, xs_off2);                                                 \
+  } while (0)
+  if (k % 4 == 0 || plan->fwd_chunk3) {
+    switch (FL) {
+      case 0: FWD_LAUNCH(4, 0); break;
+      case kFwdFlagChunk3: FWD_LAUNCH(4, kFwdFlagChunk3); break;
+      case kFwdFlagQuad: FWD_LAUNCH(4, kFwdFlagQuad); break;
+      default: FWD_LAUNCH(4, kFwdFlagChunk3 | kFwdFlagQuad); break;
     }
-  } else if ((k % 4 == 0 || plan->fwd_chunk3) && plan->fwd_acc == MAXK_ACC_F64 &&
-      plan->fwd_unroll == 8) {
-    if (FL & kFwdFlagQuad) FWD_LAUNCH_FLQ();
-    else if (W == 8) FWD_LAUNCH_FL(512);
-    else if (W == 6) FWD_LAUNCH_FL(384);
-    else FWD_LAUNCH_FL(256);
-  } else if (k % 4 == 0 && !plan->fwd_chunk3) {
-    if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(4, MAXK_ACC_F32_CAS);
-    else FWD_LAUNCH(4, MAXK_ACC_F64);
   } else {
-    if (plan->fwd_acc == MAXK_ACC_F32_CAS) FWD_LAUNCH(1, MAXK_ACC_F32_CAS);
-    else FWD_LAUNCH(1, MAXK_ACC_F64);
+    FWD_LAUNCH(1, 0);
   }
-#undef FWD_LAUNCH_FL
-#undef FWD_LAUNCH_FLQ
 #undef FWD_LAUNCH
-#undef FWD_LAUNCH1
   MAXK_LAUNCH_CHECK("spgemm_fwd launch");
   return MAXK_OK;
 }
@@ -1796,8 +1227,8 @@ extern "C" int maxk_spgemm_forward(const maxk_plan* plan, const int32_t* ptr,
                                    const int32_t* idx, const float* val,
                                    const float* sp_data, const uint8_t* sp_index, float* out,
                                    int32_t N, int64_t E, int32_t k, int32_t D, void* stream) {
-  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream, 0,
-                             nullptr, 0);
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, 0, sp_index, 0, out, N, E, k, D,
+                             stream, 0, nullptr, 0);
 }
 
 extern "C" int maxk_spgemm_forward_ws(const maxk_plan* plan, const int32_t* ptr,
@@ -1808,8 +1239,8 @@ extern "C" int maxk_spgemm_forward_ws(const maxk_plan* plan, const int32_t* ptr,
                                       int64_t workspace_bytes, void* stream) {
   MAXK_CHECK_ARG(accumulate == 0 || accumulate == 1,
                  "maxk_spgemm_forward_ws: accumulate must be 0 or 1");
-  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream,
-                             accumulate, workspace, workspace_bytes);
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, 0, sp_index, 0, out, N, E, k, D,
+                             stream, accumulate, workspace, workspace_bytes);
 }
 
 extern "C" int maxk_spgemm_forward_ex(const maxk_plan* plan, const int32_t* ptr,
@@ -1821,17 +1252,36 @@ extern "C" int maxk_spgemm_forward_ex(const maxk_plan* plan, const int32_t* ptr,
                                       int64_t workspace_bytes, void* stream) {
   MAXK_CHECK_ARG(accumulate == 0 || accumulate == 1,
                  "maxk_spgemm_forward_ex: accumulate must be 0 or 1");
-  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream,
-                             accumulate, workspace, workspace_bytes, stats, n_stats,
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, 0, sp_index, 0, out, N, E, k, D,
+                             stream, accumulate, workspace, workspace_bytes, stats, n_stats,
                              stats_stride);
 }
 
-extern "C" int maxk_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int32_t num_rows,
-                               int32_t dim_k, uint32_t* stats, void* stream) {
+extern "C" int maxk_spgemm_forward_tables(const maxk_plan* plan, const int32_t* ptr,
+                                          const int32_t* idx, const float* val,
+                                          const float* sp_data, int64_t data_stride,
+                                          const uint8_t* sp_index, int64_t index_stride,
+                                          float* out, int32_t N, int64_t E, int32_t k, int32_t D,
+                                          int32_t accumulate, const uint32_t* stats,
+                                          int32_t n_stats, int64_t stats_stride,
+                                          void* workspace, int64_t workspace_bytes,
+                                          void* stream) {
+  MAXK_CHECK_ARG(accumulate == 0 || accumulate == 1,
+                 "maxk_spgemm_forward_tables: accumulate must be 0 or 1");
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, data_stride, sp_index, index_stride,
+                             out, N, E, k, D, stream, accumulate, workspace, workspace_bytes,
+                             stats, n_stats, stats_stride);
+}
+
+extern "C" int maxk_cbsr_stats_tables(const float* sp_data, int64_t data_stride,
+                                      const uint8_t* sp_index, int64_t index_stride,
+                                      int32_t num_rows, int32_t dim_k, uint32_t* stats,
+                                      void* stream) {
   MAXK_CHECK_ARG(num_rows >= 0 && dim_k >= 1 && dim_k <= kMaxDim,
                  "maxk_cbsr_stats: bad size");
   MAXK_CHECK_ARG(stats != nullptr && (num_rows == 0 || (sp_data && sp_index)),
                  "maxk_cbsr_stats: null pointer");
+  if (int rc = table_strides(data_stride, index_stride, dim_k, "maxk_cbsr_stats")) return rc;
   hipStream_t s = (hipStream_t)stream;
   MAXK_HIP_TRY(hipMemsetAsync(stats, 0, 2 * sizeof(uint32_t), s));
   if (num_rows == 0) return MAXK_OK;
@@ -1840,7 +1290,13 @@ extern "C" int maxk_cbsr_stats(const float* sp_data, const uint8_t* sp_index, in
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  return launch_cbsr_stats(sp_data, sp_index, num_rows, dim_k, stats, stats + 1, cus, s);
+  return launch_cbsr_stats(sp_data, (int)data_stride, sp_index, (int)index_stride, num_rows,
+                           dim_k, stats, stats + 1, cus, s);
+}
+
+extern "C" int maxk_cbsr_stats(const float* sp_data, const uint8_t* sp_index, int32_t num_rows,
+                               int32_t dim_k, uint32_t* stats, void* stream) {
+  return maxk_cbsr_stats_tables(sp_data, 0, sp_index, 0, num_rows, dim_k, stats, stream);
 }
 
 extern "C" int maxk_spgemm_forward_acc(const maxk_plan* plan, const int32_t* ptr,
@@ -1848,23 +1304,27 @@ extern "C" int maxk_spgemm_forward_acc(const maxk_plan* plan, const int32_t* ptr
                                        const float* sp_data, const uint8_t* sp_index,
                                        float* out, int32_t N, int64_t E, int32_t k, int32_t D,
                                        void* stream) {
-  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, sp_index, out, N, E, k, D, stream, 1,
-                             nullptr, 0);
+  return spgemm_forward_impl(plan, ptr, idx, val, sp_data, 0, sp_index, 0, out, N, E, k, D,
+                             stream, 1, nullptr, 0);
 }
 
 static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const int32_t* idx,
                                const float* val, const float* grad_out,
-                               const uint8_t* sp_index, float* grad_sp, int32_t N, int64_t E,
-                               int32_t k, int32_t D, void* stream, void* ws, int64_t ws_bytes) {
+                               const uint8_t* sp_index, int64_t is64, float* grad_sp, int32_t N,
+                               int64_t E, int32_t k, int32_t D, void* stream, void* ws,
+                               int64_t ws_bytes) {
   (void)val;  // the plan holds the block-major snapshot of val
   MAXK_CHECK_ARG(N >= 0 && E >= 0, "maxk_sspmm_backward: negative size");
   MAXK_CHECK_ARG(D >= 1 && D <= kMaxDim, "maxk_sspmm_backward: dim_origin must be in [1, 256]");
   MAXK_CHECK_ARG(k >= 1 && k <= D, "k must be between 1 and input dimension");
+  int64_t ds_unused = 0;
+  if (int rc = table_strides(ds_unused, is64, k, "maxk_sspmm_backward")) return rc;
+  const int is = (int)is64;
   int rc = check_plan(plan, ptr, idx, N, E, k, D, "maxk_sspmm_backward");
   if (rc) return rc;
   if (N == 0) return MAXK_OK;
   MAXK_CHECK_ARG(grad_out && sp_index && grad_sp, "maxk_sspmm_backward: null pointer");
-  // per-call scratch: selector words + flush slabs (column kernels) or the E x k products
+  // per-call scratch: selector words + flush slabs (column blocks) or the E x k products
   // (two-pass)
   uint32_t* sel_ws = plan->bwd_sel;
   float* tbuf_ws = plan->bwd_tbuf;
@@ -1877,42 +1337,21 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     set_error("maxk_sspmm_backward: the plan has an external workspace; use maxk_sspmm_backward_ws");
     return MAXK_ERR_INVALID_ARG;
   }
-  float* slab = plan->bwd_slab_floats > 0
-                    ? reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(sel_ws) + plan->bwd_slab_off)
-                    : nullptr;
-  auto combine = [&]() -> int {
-    if (!slab) return MAXK_OK;
-    const int slices = (plan->bwd_block_cols * k + kCombineSlice - 1) / kCombineSlice;
-    hipLaunchKernelGGL(bwd_combine_kernel, dim3(slices, plan->n_bwd_combine), dim3(256), 0,
-                       (hipStream_t)stream, grad_sp, slab, plan->bwd_combine, k,
-                       plan->bwd_block_cols * k, plan->bwd_corder);
-    MAXK_LAUNCH_CHECK("bwd_combine launch");
-    return MAXK_OK;
-  };
   hipStream_t s = (hipStream_t)stream;
+  const int NC = plan->num_cols;
   if (plan->bwd_twopass) {
     // the plan checked k % 4 == 0, k / 4 a power of two <= 64, E > 0, NC > 0; per row chunk
     // (the workspace holds one chunk's products): row pass, then column pass
     const int R = plan->bwd_tp_rows;
-    const bool cs = plan->bwd_tp_csc;  // the plan allows it with one chunk only
     const int P = plan->bwd_tp_chunks;
-    const int NC = plan->num_cols;
     for (int p = 0; p < P; ++p) {
       const int rb = plan->tp_rows[p], re = plan->tp_rows[p + 1];
       const int64_t eb = plan->tp_edges[p];
       if (re > rb) {
         const dim3 rgrid((re - rb + 4 * R - 1) / (4 * R));
-#define ROWS_LAUNCH(RR)                                                                   \
-        do {                                                                              \
-          if (cs)                                                                         \
-            hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR, true>), rgrid, dim3(256), 0, s, \
-                               ptr, plan->bwd_erec, grad_out, sp_index, tbuf_ws, rb, re,  \
-                               eb, D, k, plan->bwd_perm);                                 \
-          else                                                                            \
-            hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR>), rgrid, dim3(256), 0, s, ptr, \
-                               plan->bwd_erec, grad_out, sp_index, tbuf_ws, rb, re, eb, D, \
-                               k, nullptr);                                               \
-        } while (0)
+#define ROWS_LAUNCH(RR)                                                                     \
+        hipLaunchKernelGGL((sspmm_bwd_rows_kernel<4, RR>), rgrid, dim3(256), 0, s, ptr,    \
+                           plan->bwd_erec, grad_out, sp_index, is, tbuf_ws, rb, re, eb, D, k)
         if (R >= 8) ROWS_LAUNCH(8);
         else if (R == 4) ROWS_LAUNCH(4);
         else if (R == 2) ROWS_LAUNCH(2);
@@ -1922,184 +1361,69 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       }
       const int32_t* lo = P > 1 ? plan->bwd_colptr2 + (size_t)p * NC : plan->bwd_colptr;
       const int32_t* hi = P > 1 ? plan->bwd_colptr2 + (size_t)(p + 1) * NC : plan->bwd_colptr + 1;
-      if (cs)
-        hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4, true>), dim3((NC + 3) / 4), dim3(256), 0, s,
-                           lo, hi, nullptr, tbuf_ws, (int64_t)0, grad_sp, NC, k, 0);
-      else
-        hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4>), dim3((NC + 3) / 4), dim3(256), 0, s, lo,
-                           hi, plan->bwd_perm, tbuf_ws, eb, grad_sp, NC, k, p > 0 ? 1 : 0);
+      hipLaunchKernelGGL((sspmm_bwd_cols_kernel<4>), dim3((NC + 3) / 4), dim3(256), 0, s, lo, hi,
+                         plan->bwd_perm, tbuf_ws, eb, grad_sp, NC, k, p > 0 ? 1 : 0);
       MAXK_LAUNCH_CHECK("sspmm_bwd_cols launch");
     }
     return MAXK_OK;
   }
-  if (plan->bwd_csc) {
-    const int F = plan->bwd_feats;
-    if (F == 4) {
-      const int nsel = plan->num_cols * (k / 4);
-      hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
-                         plan->num_cols, k, 1, sel_ws, nullptr);
-    }
-    const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
-    const dim3 cgrid((plan->num_cols + 3) / 4);
-#define CSC_LAUNCH(FF, UU)                                                                \
-    hipLaunchKernelGGL((sspmm_bwd_csc_kernel<FF, UU>), cgrid, dim3(256), 0, s,            \
-                       plan->bwd_colptr, plan->bwd_rec, grad_out, g_bytes, sel_ws, \
-                       sp_index, grad_sp, plan->num_cols, k)
-    if (F == 4) {
-      if (plan->bwd_unroll >= 8) CSC_LAUNCH(4, 8);
-      else CSC_LAUNCH(4, 4);
-    } else {
-      if (plan->bwd_unroll >= 16) CSC_LAUNCH(1, 16);
-      else if (plan->bwd_unroll >= 8) CSC_LAUNCH(1, 8);
-      else CSC_LAUNCH(1, 4);
-    }
-#undef CSC_LAUNCH
-    MAXK_LAUNCH_CHECK("sspmm_bwd_csc launch");
-    return MAXK_OK;
-  }
-  if (plan->n_bwd_shared > 0 && !slab)  // atomic flush: shared blocks add into zeros
-    MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)plan->num_cols * k * sizeof(float), s));
+  float* slab = plan->bwd_slab_floats > 0
+                    ? reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(sel_ws) + plan->bwd_slab_off)
+                    : nullptr;
+  // no edges: no tasks, every gradient is zero; atomic flush: split blocks add into zeros
+  if (plan->n_bwd_tasks == 0 || (plan->n_bwd_shared > 0 && !slab))
+    MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)NC * k * sizeof(float), s));
   if (plan->n_bwd_tasks == 0) return MAXK_OK;
-  const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, k, plan->bwd_acc);
-  const dim3 grid(plan->n_bwd_tasks), block(kBwdThreads);  // general path: 512 threads
-  if (plan->bwd_rec && plan->bwd_feats == 1) {
-    const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
-    const size_t lds1 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
-                        (size_t)plan->bwd_block_cols * k;
-#define BWD1_LAUNCH(UU, NT)                                                               \
-    do {                                                                                  \
-      if (lds1 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd1_kernel<UU, NT>, lds1));     \
-      hipLaunchKernelGGL((sspmm_bwd1_kernel<UU, NT>), grid, dim3(NT), lds1, s,            \
-                         plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sp_index,     \
-                         grad_sp, k, plan->bwd_ks, slab, plan->bwd_corder);              \
-    } while (0)
-    const int W = plan->bwd_waves, U = plan->bwd_unroll;
-    if (W == 16) BWD1_LAUNCH(16, 1024);
-    else if (W == 12) {
-      if (U >= 16) BWD1_LAUNCH(16, 768);
-      else BWD1_LAUNCH(8, 768);
-    } else if (U >= 16) BWD1_LAUNCH(16, 512);
-    else if (U >= 12) BWD1_LAUNCH(12, 512);
-    else BWD1_LAUNCH(8, 512);
-#undef BWD1_LAUNCH
-    MAXK_LAUNCH_CHECK("sspmm_bwd1 launch");
-    return combine();
-  }
-  if (plan->bwd_rec && plan->bwd_feats == 2) {  // two slots per lane
-    const int S = plan->bwd_slot_groups;
-    const int nsel = plan->num_cols * (k / 2);
-    hipLaunchKernelGGL(pack_sel2_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
-                       plan->num_cols, k, S, reinterpret_cast<uint16_t*>(sel_ws),
+  const int F = plan->bwd_feats, S = plan->bwd_slot_groups, ns = plan->bwd_ks;
+  const int L = ns / F;
+  const int nsel = NC * L * S;
+  if (F == 4)
+    hipLaunchKernelGGL(pack_sel_kernel<4>, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index, is,
+                       NC, k, plan->bwd_kp, S, sel_ws, plan->bwd_corder);
+  else
+    hipLaunchKernelGGL(pack_sel_kernel<2>, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index, is,
+                       NC, k, plan->bwd_kp, S, reinterpret_cast<uint16_t*>(sel_ws),
                        plan->bwd_corder);
-    const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
-    const size_t lds2 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
-                        (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
-#define BWD2_LAUNCH(UU, NT, V, Q)                                                         \
-    do {                                                                                  \
-      if (lds2 > 64 * 1024)                                                               \
-        MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, false, V, Q, 2>, lds2));         \
-      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, false, V, Q, 2>), grid, dim3(NT), lds2, s, \
-                         plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sel_ws,       \
-                         grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds,  \
-                         slab, plan->bwd_corder);                                         \
-    } while (0)
-    const int U = plan->bwd_unroll;
-    const bool QL = plan->bwd_quad && (k / S / 2) % 4 == 0;
-    if (plan->bwd_cas64) {
-      if (U >= 16) {
-        if (QL) BWD2_LAUNCH(16, 512, true, true);
-        else BWD2_LAUNCH(16, 512, true, false);
-      } else if (U >= 12) {
-        if (QL) BWD2_LAUNCH(12, 512, true, true);
-        else BWD2_LAUNCH(12, 512, true, false);
-      } else {
-        if (QL) BWD2_LAUNCH(8, 512, true, true);
-        else BWD2_LAUNCH(8, 512, true, false);
-      }
-    } else {
-      if (QL) BWD2_LAUNCH(8, 512, false, true);
-      else BWD2_LAUNCH(8, 512, false, false);
-    }
-#undef BWD2_LAUNCH
-    MAXK_LAUNCH_CHECK("sspmm_bwd2 launch");
-    return combine();
-  }
-  if (plan->bwd_rec) {
-    const int S = plan->bwd_slot_groups;
-    const int nsel = plan->num_cols * (k / 4);
-    hipLaunchKernelGGL(pack_sel_kernel, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index,
-                       plan->num_cols, k, S, sel_ws, plan->bwd_corder);
-    const uint32_t g_bytes = (uint32_t)((uint64_t)N * D * 4u);
-    const size_t lds4 = ((size_t)plan->bwd_block_cols * plan->bwd_ks + 3) / 4 * 4 * sizeof(float) +
-                        (plan->bwd_sel_lds ? (size_t)plan->bwd_block_cols * (k / S) : 0);
-#define BWD4_LAUNCH(UU, NT, PF, V, Q)                                                     \
-    do {                                                                                  \
-      if (lds4 > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, PF, V, Q>, lds4)); \
-      hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, PF, V, Q>), grid, dim3(NT), lds4, s,  \
-                         plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, sel_ws, \
-                         grad_sp, k, S, plan->num_cols, plan->bwd_ks, plan->bwd_sel_lds,  \
-                         slab, plan->bwd_corder);                                         \
-    } while (0)
-    const int W = plan->bwd_waves, U = plan->bwd_unroll;
-    const bool PFon = plan->bwd_prefetch != 0;
-    const bool QL = plan->bwd_quad && (k / S / 4) % 4 == 0;  // quad-aligned edge lane groups
-    if (plan->bwd_cas64) {
-      if (W == 16) {
-        if (QL) BWD4_LAUNCH(6, 1024, false, true, true);
-        else BWD4_LAUNCH(6, 1024, false, true, false);
-      } else if (W == 12) {
-        if (QL) BWD4_LAUNCH(8, 768, false, true, true);
-        else BWD4_LAUNCH(8, 768, false, true, false);
-      } else if (PFon) {
-        if (QL) BWD4_LAUNCH(8, 512, true, true, true);
-        else BWD4_LAUNCH(8, 512, true, true, false);
-      } else if (U == 12) {
-        if (QL) BWD4_LAUNCH(12, 512, false, true, true);
-        else BWD4_LAUNCH(12, 512, false, true, false);
-      } else if (U == 16) {
-        BWD4_LAUNCH(16, 512, false, true, false);
-      } else {
-        if (QL) BWD4_LAUNCH(8, 512, false, true, true);
-        else BWD4_LAUNCH(8, 512, false, true, false);
-      }
-    } else if (W == 16) {
-      if (PFon) BWD4_LAUNCH(6, 1024, true, false, false);
-      else BWD4_LAUNCH(6, 1024, false, false, false);
-    } else if (W == 12) {
-      if (PFon) BWD4_LAUNCH(8, 768, true, false, false);
-      else BWD4_LAUNCH(8, 768, false, false, false);
-    } else if (PFon) {
-      BWD4_LAUNCH(8, 512, true, false, false);
-    } else if (U == 16) BWD4_LAUNCH(16, 512, false, false, false);
-    else if (U == 12) BWD4_LAUNCH(12, 512, false, false, false);
-    else if (U == 4) BWD4_LAUNCH(4, 512, false, false, false);
-    else BWD4_LAUNCH(8, 512, false, false, false);
-#undef BWD4_LAUNCH
-    MAXK_LAUNCH_CHECK("sspmm_bwd launch");
-    return combine();
-  }
-#define BWD_LAUNCH1(F, A, UU)                                                             \
-  do {                                                                                    \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd_kernel<F, A, UU>, lds));       \
-    hipLaunchKernelGGL((sspmm_bwd_kernel<F, A, UU>), grid, block, lds, s, plan->bwd_tasks, \
-                       plan->bwd_row, plan->bwd_col, plan->bwd_val, grad_out, sp_index,   \
-                       grad_sp, D, k);                                                    \
+  MAXK_LAUNCH_CHECK("pack_sel launch");
+  const uint32_t g_bytes = plan->bwd_big ? 0u : (uint32_t)((uint64_t)N * D * 4u);
+  const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, ns);
+  const dim3 grid(plan->n_bwd_tasks);
+  const bool Q = L % 4 == 0;  // quad-aligned lane groups: batched record loads
+  const int U = plan->bwd_unroll, W = plan->bwd_waves;
+#define BWD_LAUNCH(UU, NT, FF, QQ, BB)                                                      \
+  do {                                                                                      \
+    using SelT = std::conditional_t<FF == 4, uint32_t, uint16_t>;                          \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, FF, QQ, BB>, lds)); \
+    hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, FF, QQ, BB>), grid, dim3(NT), lds, s,     \
+                       plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, D,                \
+                       reinterpret_cast<const SelT*>(sel_ws), grad_sp, k, ns, NC, slab,     \
+                       plan->bwd_corder);                                                   \
   } while (0)
-#define BWD_LAUNCH(F, A)                                                                  \
-  do {                                                                                    \
-    if (plan->bwd_unroll >= 12) BWD_LAUNCH1(F, A, 16);                                    \
-    else BWD_LAUNCH1(F, A, 8);                                                            \
+#define BWD_SHAPES(FF, QQ)                                                                  \
+  do {                                                                                      \
+    if (plan->bwd_big) BWD_LAUNCH(8, 512, FF, QQ, true);                                    \
+    else if (W == 12) BWD_LAUNCH(8, 768, FF, QQ, false);                                    \
+    else if (U == 16) BWD_LAUNCH(16, 512, FF, QQ, false);                                   \
+    else if (U == 12) BWD_LAUNCH(12, 512, FF, QQ, false);                                   \
+    else BWD_LAUNCH(8, 512, FF, QQ, false);                                                 \
   } while (0)
-  if (plan->bwd_feats == 4) {
-    if (plan->bwd_acc == MAXK_ACC_F32_CAS) BWD_LAUNCH(4, MAXK_ACC_F32_CAS);
-    else BWD_LAUNCH(4, MAXK_ACC_F64);
+  if (F == 4) {
+    if (Q) BWD_SHAPES(4, true);
+    else BWD_SHAPES(4, false);
   } else {
-    if (plan->bwd_acc == MAXK_ACC_F32_CAS) BWD_LAUNCH(1, MAXK_ACC_F32_CAS);
-    else BWD_LAUNCH(1, MAXK_ACC_F64);
+    if (Q) BWD_SHAPES(2, true);
+    else BWD_SHAPES(2, false);
   }
+#undef BWD_SHAPES
 #undef BWD_LAUNCH
-#undef BWD_LAUNCH1
   MAXK_LAUNCH_CHECK("sspmm_bwd launch");
+  if (slab) {
+    const int slices = (plan->bwd_block_cols * k + kCombineSlice - 1) / kCombineSlice;
+    hipLaunchKernelGGL(bwd_combine_kernel, dim3(slices, plan->n_bwd_combine), dim3(256), 0, s,
+                       grad_sp, slab, plan->bwd_combine, k, plan->bwd_block_cols * k,
+                       plan->bwd_corder);
+    MAXK_LAUNCH_CHECK("bwd_combine launch");
+  }
   return MAXK_OK;
 }
 
@@ -2108,7 +1432,7 @@ extern "C" int maxk_sspmm_backward(const maxk_plan* plan, const int32_t* ptr,
                                    const float* grad_out, const uint8_t* sp_index,
                                    float* grad_sp, int32_t N, int64_t E, int32_t k, int32_t D,
                                    void* stream) {
-  return sspmm_backward_impl(plan, ptr, idx, val, grad_out, sp_index, grad_sp, N, E, k, D,
+  return sspmm_backward_impl(plan, ptr, idx, val, grad_out, sp_index, 0, grad_sp, N, E, k, D,
                              stream, nullptr, 0);
 }
 
@@ -2118,8 +1442,18 @@ extern "C" int maxk_sspmm_backward_ws(const maxk_plan* plan, const int32_t* ptr,
                                       float* grad_sp, int32_t N, int64_t E, int32_t k,
                                       int32_t D, void* workspace, int64_t workspace_bytes,
                                       void* stream) {
-  return sspmm_backward_impl(plan, ptr, idx, val, grad_out, sp_index, grad_sp, N, E, k, D,
+  return sspmm_backward_impl(plan, ptr, idx, val, grad_out, sp_index, 0, grad_sp, N, E, k, D,
                              stream, workspace, workspace_bytes);
+}
+
+extern "C" int maxk_sspmm_backward_tables(const maxk_plan* plan, const int32_t* ptr,
+                                          const int32_t* idx, const float* val,
+                                          const float* grad_out, const uint8_t* sp_index,
+                                          int64_t index_stride, float* grad_sp, int32_t N,
+                                          int64_t E, int32_t k, int32_t D, void* workspace,
+                                          int64_t workspace_bytes, void* stream) {
+  return sspmm_backward_impl(plan, ptr, idx, val, grad_out, sp_index, index_stride, grad_sp, N,
+                             E, k, D, stream, workspace, workspace_bytes);
 }
 
 extern "C" int maxk_dense_spmm_csr(const int32_t* ptr, const int32_t* idx, const float* val,

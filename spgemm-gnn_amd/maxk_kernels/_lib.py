@@ -25,6 +25,8 @@ SIGNATURES = {
     "maxk_last_error": (ctypes.c_char_p, []),
     "maxk_topk_cbsr": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "maxk_topk_cbsr_count": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
+    "maxk_topk_cbsr_tables": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32,
+                                             _i32, _vp]),
     "maxk_scatter_backward": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "maxk_plan_create": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp,
                                         ctypes.POINTER(_vp)]),
@@ -39,6 +41,12 @@ SIGNATURES = {
     "maxk_plan_get_info_sized": (ctypes.c_int, [_vp, _vp, _i64]),
     "maxk_plan_get_col_order": (ctypes.c_int, [_vp, _vp, _vp]),
     "maxk_cbsr_stats": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp]),
+    "maxk_cbsr_stats_tables": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i32, _i32, _vp, _vp]),
+    "maxk_spgemm_forward_tables": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp,
+                                                  _i32, _i64, _i32, _i32, _i32, _vp, _i32, _i64,
+                                                  _vp, _i64, _vp]),
+    "maxk_sspmm_backward_tables": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i32,
+                                                  _i64, _i32, _i32, _vp, _i64, _vp]),
     "maxk_spgemm_forward_ex": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64,
                                               _i32, _i32, _i32, _vp, _i32, _i64, _vp, _i64,
                                               _vp]),
@@ -61,7 +69,8 @@ SIGNATURES = {
 
 
 class PlanOptions(ctypes.Structure):
-    """Mirror of ``maxk_plan_options`` (0 = default for every field)."""
+    """Mirror of ``maxk_plan_options`` (0 = default for every field; the fields the header
+    marks "ABI 3" accept only 0 or the behaviour that remains)."""
 
     _fields_ = [
         ("fwd_tile_rows", _i32),
@@ -109,8 +118,10 @@ class PlanOptions(ctypes.Structure):
 
 
 ACC_KINDS = {"auto": 0, "f64": 1, "f32_cas": 2}
-# maxk_plan_options.col_order by name
-COL_ORDERS = {"auto": 0, "identity": 1, "scattered": 2, "clustered": 3, "given": 4}
+# maxk_plan_options.col_order by name (MAXK_COL_ORDER_*; 3, clustered, was removed in ABI 3)
+COL_ORDERS = {"auto": 0, "identity": 1, "scattered": 2, "given": 4}
+# maxk_plan_options.bwd_algo / maxk_plan_info.bwd_algo (MAXK_BWD_*)
+BWD_ALGOS = {"auto": 0, "column_blocks": 1, "two_pass": 3}
 
 
 class PlanInfo(ctypes.Structure):

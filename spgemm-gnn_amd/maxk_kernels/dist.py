@@ -7,54 +7,56 @@ exchange per direction:
 * partition: contiguous row ranges balanced by nnz; rank q owns rows [start_q, end_q),
   their CSR slice (columns keep pointing at any node) and computes the top-k of its own
   rows (weights are replicated);
-* forward : RCCL all-gathers of the k-sparse CBSR block (sp_data f32 and sp_index u8)
-  straight into the tables the kernels read; the rank's top-k can be written directly into
-  its send buffers (``local_buffers``), so the exchange moves no extra copies. Then the
-  local SpGEMM over the rank's rows with rectangular plans whose column ids are remapped
-  into the gathered table (once, at partition time);
-* backward: the local SSpMM produces a partial grad_sp for every (padded) column; an
-  RCCL reduce-scatter (sum) returns each rank its own rows' gradient.
+* forward : ONE RCCL all-gather of the k-sparse CBSR block as interleaved records
+  {k f32 values, k u8 selectors} per row (5k bytes at k % 4 == 0), straight into the table
+  the kernels read: the forward gathers these records in place (no per-call record pack over
+  the N columns; maxk_spgemm_forward_tables) and the backward reads the selectors at the
+  record stride. The rank's top-k is written straight into its send records
+  (``local_buffers`` + maxk_topk_cbsr_tables), so the exchange moves no extra copies. Then
+  the local SpGEMM over the rank's rows with a rectangular plan whose column ids are
+  remapped into the gathered table (once, at partition time);
+* backward: the local SSpMM produces a partial grad_sp for every (padded) column; an RCCL
+  reduce-scatter (sum) returns each rank its own rows' gradient.
 
-Fixed-point statistics: with one phase, every rank's block of the table ends in a spare row.
-Before the all-gather the rank writes the fixed-point statistics of its own rows into the
-selector bytes of that row (``maxk_cbsr_stats``: two words; the value row stays zero, so the
-row adds nothing anywhere), the gathered index table carries one pair per rank and the
-forward reads those W pairs (``maxk_spgemm_forward_ex``) instead of scanning the whole table.
+Fixed-point statistics: every rank's block of the table ends in a spare row no edge points
+at. Before the all-gather the rank writes the fixed-point statistics of its own rows into the
+first 8 bytes of that record (``maxk_cbsr_stats``: two words), the gathered table carries one
+pair per rank and the forward reads those W pairs (``maxk_spgemm_forward_ex``) instead of
+scanning the whole table.
 
-Local-columns-first split (``split=True``, one phase, forward only): the rank's edges are
-cut into those whose column it owns and the rest, with a plan each. The forward runs the
-local plan on the send buffers while the all-gather is in flight, then the remote plan
-accumulates on the gathered table. The backward runs one plan over all the rank's edges and
-then the reduce-scatter: splitting it too (remote plan, reduce-scatter in flight while the
-local plan runs) cost more than the exchange it hides (Reddit k=16, one rank of W=2 / 8:
-0.88 -> 1.34 ms / 0.23 -> 0.32 ms, ``tools/shard_time.py``), since each part's column
-blocks see half as many edges per grad_out row.
-
-Column phases (``phases`` P > 1): every rank's rows are cut into P parts and the table is
-laid out phase-major (phase p holds part p of every rank), so each phase is one all-gather
-and one reduce-scatter of its own. The rank keeps one plan per phase (its edges split by the
-phase of their column). The all-gather of phase p+1 then runs while the SpGEMM of phase p
-(accumulating into the same output) computes, and the reduce-scatter of phase p while the
-SSpMM of phase p+1 computes. P = 1 is the plain one-shot exchange.
-
-Bytes exchanged per step are 5kN (all-gathers) + 4kN (reduce-scatter), i.e. 18.6 MB +
-14.9 MB for Reddit at k=16, against 238 MB for all-gathering dense features.
+Bytes exchanged per step are 5kN (all-gather) + 4kN (reduce-scatter), i.e. 18.6 MB + 14.9 MB
+for Reddit at k=16, against 238 MB for all-gathering dense features. Round 3's two
+all-gathers (values, selectors), column phases and local-columns-first split are gone: the
+phases and the split cost more compute than the exchange they could hide.
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional
+from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
 
 
-class RowPartition:
-    """Contiguous destination-row ranges with ~equal nnz per rank, and the phase-major
-    layout of the all-gathered CBSR table (``phases`` parts per rank; with one phase each
-    rank's block ends in a spare row that carries its fixed-point statistics)."""
+def record_bytes(k: int) -> int:
+    """Bytes of one interleaved CBSR record: k f32 values, then the k selector bytes padded to
+    whole words (5k at k % 4 == 0)."""
+    return 4 * k + 4 * (-(-k // 4))
 
-    def __init__(self, ptr: torch.Tensor, world_size: int, phases: int = 1,
-                 stats_row: Optional[bool] = None):
+
+def record_views(buf: torch.Tensor, k: int):
+    """(values f32 [rows, k], selectors u8 [rows, k]) strided views of a uint8 record buffer
+    [rows, record_bytes(k)]."""
+    rb = record_bytes(k)
+    assert buf.dtype == torch.uint8 and buf.dim() == 2 and buf.shape[1] == rb
+    return buf[:, :4 * k].view(torch.float32), buf[:, 4 * k:4 * k + k]
+
+
+class RowPartition:
+    """Contiguous destination-row ranges with ~equal nnz per rank, and the layout of the
+    all-gathered record table: rank q's block holds its rows at [q * block_rows, ...) and
+    ends in a spare row carrying its fixed-point statistics."""
+
+    def __init__(self, ptr: torch.Tensor, world_size: int):
         p = ptr.detach().to("cpu", torch.int64)
         n = p.numel() - 1
         e = int(p[-1])
@@ -69,168 +71,101 @@ class RowPartition:
         self.bounds = b                      # [W+1] row boundaries
         counts = b[1:] - b[:-1]
         self.max_rows = max(1, int(counts.max()))
-        self.phases = max(1, int(phases))
-        self.stats_row = (self.phases == 1) if stats_row is None else bool(stats_row)
-        if self.stats_row and self.phases != 1:
-            raise ValueError("the statistics row needs a one-phase partition")
-        self.rows_per_phase = -(-self.max_rows // self.phases)  # node rows of a rank per phase
-        self.phase_rows = self.rows_per_phase + (1 if self.stats_row else 0)
-        self.phase_cols = w * self.phase_rows                  # table rows of one phase
-        self.send_rows = self.phases * self.phase_rows         # >= max_rows
-        self.padded_rows = self.phases * self.phase_cols
+        self.block_rows = self.max_rows + 1  # + the statistics row
+        self.padded_rows = w * self.block_rows
 
     def rows(self, rank: int):
         return int(self.bounds[rank]), int(self.bounds[rank + 1])
 
-    def _position(self, q: torch.Tensor, off: torch.Tensor) -> torch.Tensor:
-        ph = off // self.rows_per_phase
-        return ph * self.phase_cols + q * self.phase_rows + (off - ph * self.rows_per_phase)
+    def edges(self, ptr: torch.Tensor, rank: int):
+        """CSR edge range [e0, e1) of rank's rows."""
+        r0, r1 = self.rows(rank)
+        return int(ptr[r0]), int(ptr[r1])
 
     def remap_columns(self, idx: torch.Tensor) -> torch.Tensor:
-        """Global column id -> position in the padded (phase-major) all-gather table."""
+        """Global column id -> position in the padded all-gather table."""
         b = self.bounds.to(idx.device)
         c = idx.to(torch.int64)
         q = torch.searchsorted(b, c, right=True) - 1
-        return self._position(q, c - b[q]).to(torch.int32)
+        return (q * self.block_rows + (c - b[q])).to(torch.int32)
 
     def table_positions(self, rank: int, device=None) -> torch.Tensor:
         """Table rows holding rank's nodes, in node order (int64 [n_rank])."""
         a, b = self.rows(rank)
-        off = torch.arange(b - a, dtype=torch.int64, device=device)
-        return self._position(torch.full_like(off, rank), off)
+        return rank * self.block_rows + torch.arange(b - a, dtype=torch.int64, device=device)
 
     def stats_position(self, rank: int) -> int:
-        """Table row of rank's statistics pair (one-phase partitions)."""
-        return rank * self.phase_rows + self.rows_per_phase
+        """Table row of rank's statistics pair."""
+        return rank * self.block_rows + self.max_rows
 
-    def local_csr(self, ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, rank: int):
-        """(ptr, remapped idx, val) of rank's rows; ptr rebased to 0."""
+    def local_csr(self, ptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, rank: int,
+                  local_edges: bool = False):
+        """(ptr rebased to 0, remapped idx, val) of rank's rows. ``local_edges``: idx / val
+        already hold only those rows' edges (a rank that generated or loaded its own rows)."""
         r0, r1 = self.rows(rank)
         e0, e1 = int(ptr[r0]), int(ptr[r1])
         lptr = (ptr[r0:r1 + 1].to(torch.int64) - e0).to(torch.int32).contiguous()
-        lidx = self.remap_columns(idx[e0:e1]).contiguous()
-        lval = val[e0:e1].contiguous()
-        return lptr, lidx, lval
-
-    def phase_csr(self, lptr: torch.Tensor, lidx: torch.Tensor, lval: torch.Tensor, phase: int):
-        """The edges of a local CSR (remapped columns) whose column lies in ``phase``, with
-        columns rebased to that phase's table block [0, phase_cols)."""
-        lo = phase * self.phase_cols
-        return select_csr(lptr, lidx, lval, (lidx >= lo) & (lidx < lo + self.phase_cols), lo)
+        if not local_edges:
+            idx, val = idx[e0:e1], val[e0:e1]
+        assert idx.numel() == e1 - e0 and val.numel() == e1 - e0, "edges of the wrong rows"
+        return lptr, self.remap_columns(idx).contiguous(), val.contiguous()
 
 
-def select_csr(lptr: torch.Tensor, lidx: torch.Tensor, lval: torch.Tensor,
-               keep: torch.Tensor, shift: int = 0):
-    """The edges of a CSR where ``keep`` holds (row order kept), columns minus ``shift``."""
-    n = lptr.numel() - 1
-    rows = torch.repeat_interleave(torch.arange(n, device=lptr.device),
-                                   (lptr[1:] - lptr[:-1]).to(torch.int64))
-    cnt = torch.bincount(rows[keep], minlength=n)
-    pptr = torch.zeros(n + 1, dtype=torch.int64, device=lptr.device)
-    pptr[1:] = torch.cumsum(cnt, 0)
-    return (pptr.to(torch.int32).contiguous(), (lidx[keep] - shift).to(torch.int32).contiguous(),
-            lval[keep].contiguous())
-
-
-# injected per-part compute (CPU tests): fwd(part, table_data, table_index, out) -> out (out
-# is None for the first part, else the output to accumulate into); bwd(part, grad_out,
-# table_index) -> the part's grad rows. A part reads the table given by ShardedAggregation
-# (its phase's block, or for the split: the send buffers / the whole table).
-FwdFn = Callable[[int, torch.Tensor, torch.Tensor, Optional[torch.Tensor]], torch.Tensor]
-BwdFn = Callable[[int, torch.Tensor, torch.Tensor], torch.Tensor]
+# injected per-rank compute (CPU tests): fwd(table_data, table_index, out=None) -> out [n_local,
+# D]; bwd(grad_out [n_local, D], table_index) -> grad for every table row [padded_rows, k].
+FwdFn = Callable[[torch.Tensor, torch.Tensor], torch.Tensor]
+BwdFn = Callable[[torch.Tensor, torch.Tensor], torch.Tensor]
 
 
 class ShardedAggregation:
     """One rank's share of Y = A densify(sp) and of its SSpMM backward.
 
-    ``fwd``/``bwd`` default to the gfx950 kernels through one rectangular GraphPlan per
-    part (``plan_options``: the same knobs as ``GraphPlan(options=...)``, e.g.
+    ``fwd``/``bwd`` default to the gfx950 kernels through one rectangular GraphPlan
+    (``plan_options``: the same knobs as ``GraphPlan(options=...)``, e.g.
     ``{"bwd_algo": 3}``); tests on CPU (gloo) inject checker callables to exercise the
-    partition, the layouts and the collectives. ``parts[i]`` = (ptr, idx, val, num_cols) of
-    part i: the column phases, or (split) the own-column and the remote-column edges.
+    partition, the record layout and the collectives.
     """
 
     def __init__(self, part: RowPartition, rank: int, ptr: torch.Tensor, idx: torch.Tensor,
                  val: torch.Tensor, dim_origin: int, dim_k: int,
                  group: Optional[dist.ProcessGroup] = None, fwd: Optional[FwdFn] = None,
                  bwd: Optional[BwdFn] = None, plan_options: Optional[dict] = None,
-                 split: bool = False):
+                 local_edges: bool = False):
         self.part, self.rank, self.group = part, rank, group
         self.dim_origin, self.dim_k = int(dim_origin), int(dim_k)
         self.r0, self.r1 = part.rows(rank)
         self.n_local = self.r1 - self.r0
-        self.ptr, self.idx, self.val = part.local_csr(ptr, idx, val, rank)
+        self.ptr, self.idx, self.val = part.local_csr(ptr, idx, val, rank, local_edges)
         dev = self.ptr.device
-        P, k = part.phases, self.dim_k
-        if split and P != 1:
-            raise ValueError("the local-columns-first split needs a one-phase partition")
-        self.split = bool(split)
-        # padded send buffers (rows >= n_local stay zero) and the all-gathered tables
-        self.send_data = torch.zeros((part.send_rows, k), dtype=torch.float32, device=dev)
-        self.send_index = torch.zeros((part.send_rows, k), dtype=torch.uint8, device=dev)
-        self.table_data = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
-        self.table_index = torch.empty((part.padded_rows, k), dtype=torch.uint8, device=dev)
+        k = self.dim_k
+        rb = record_bytes(k)
+        # send block (rows >= n_local stay zero; the last row carries the statistics) and the
+        # all-gathered table, both interleaved records
+        self.send_rec = torch.zeros((part.block_rows, rb), dtype=torch.uint8, device=dev)
+        self.table_rec = torch.zeros((part.padded_rows, rb), dtype=torch.uint8, device=dev)
+        self.send_data, self.send_index = record_views(self.send_rec, k)
+        self.table_data, self.table_index = record_views(self.table_rec, k)
         self.grad_table = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
-        self.grad_local = torch.empty((part.send_rows, k), dtype=torch.float32, device=dev)
-        if self.split:
-            lo = rank * part.phase_rows
-            own = (self.idx >= lo) & (self.idx < lo + self.n_local)
-            # own columns, remote columns (forward), all edges (backward)
-            self.parts = [select_csr(self.ptr, self.idx, self.val, own, lo) + (max(1, self.n_local),),
-                          select_csr(self.ptr, self.idx, self.val, ~own) + (part.padded_rows,),
-                          (self.ptr, self.idx, self.val, part.padded_rows)]
-        else:
-            self.parts = [part.phase_csr(self.ptr, self.idx, self.val, p) + (part.phase_cols,)
-                          for p in range(P)]
-        self.plans: List = []
+        self.grad_local = torch.empty((part.block_rows, k), dtype=torch.float32, device=dev)
+        self.plan = None
         native = fwd is None or bwd is None
         if native:
             from .ops import GraphPlan
-            for pp, pi, pv, nc in self.parts:
-                self.plans.append(GraphPlan(pp, pi, pv, self.n_local, pi.numel(),
-                                            self.dim_origin, self.dim_k, num_cols=nc,
-                                            options=plan_options))
-        # the statistics pair in the selector bytes of the send buffer's spare row (one
-        # phase, native kernels; 4-byte aligned words: k % 4 == 0, k >= 8)
-        self.stats = native and part.stats_row and k % 4 == 0 and k >= 8
-        rp = part.rows_per_phase
-        self._stats_local = (self._words(self.send_index, rp), 1, 2) if self.stats else None
-        self._stats_all = ((self._words(self.table_index, rp), part.world_size,
-                            part.phase_rows * k // 4) if self.stats else None)
-        self._fwd = fwd or self._native_fwd
-        self._bwd = bwd or (lambda i, g, ti: self.plans[i].backward(g, ti, self._grad_dst(i)))
-
-    @staticmethod
-    def _words(index_table: torch.Tensor, row: int) -> torch.Tensor:
-        """int32 view of a u8 table from ``row`` on (the statistics words of a spare row)."""
-        return index_table[row:].view(-1).view(torch.int32)
-
-    def _native_fwd(self, i, td, ti, out):
-        stats = None
-        if self.stats:
-            stats = self._stats_local if (self.split and i == 0) else self._stats_all
-        return self.plans[i].forward(td, ti, out, accumulate=out is not None, stats=stats)
-
-    def _grad_dst(self, i):
-        if self.split:
-            return self.grad_table
-        return self._slice(self.grad_table, i)
-
-    @property
-    def plan(self):
-        """The plan of a one-part partition (bench.py's per-kernel timing)."""
-        return self.plans[0] if len(self.plans) == 1 else None
-
-    def _slice(self, table: torch.Tensor, p: int) -> torch.Tensor:
-        c = self.part.phase_cols
-        return table[p * c: (p + 1) * c]
-
-    def _send_slice(self, buf: torch.Tensor, p: int) -> torch.Tensor:
-        r = self.part.phase_rows
-        return buf[p * r: (p + 1) * r]
+            self.plan = GraphPlan(self.ptr, self.idx, self.val, self.n_local, self.idx.numel(),
+                                  self.dim_origin, k, num_cols=part.padded_rows,
+                                  options=plan_options)
+        # the statistics pair in the first 8 bytes of each block's spare record
+        self.stats = native
+        words = rb // 4
+        self._stats_words_send = self.send_rec.view(torch.int32)[part.max_rows, :2]
+        self._stats_all = (self.table_rec.view(torch.int32).view(-1)[part.max_rows * words:],
+                           part.world_size, part.block_rows * words)
+        self._fwd = fwd or (lambda td, ti, out=None: self.plan.forward(td, ti, out,
+                                                                       stats=self._stats_all))
+        self._bwd = bwd or (lambda g, ti: self.plan.backward(g, ti, self.grad_table))
 
     def local_buffers(self):
-        """(sp_data, sp_index) views [n_local, k] of the send buffers: write this rank's
+        """(sp_data, sp_index) strided views [n_local, k] of the send records: write this rank's
         top-k here (``maxk_forward(h, k, out=...)``) and ``gather`` sends them as they are."""
         return self.send_data[: self.n_local], self.send_index[: self.n_local]
 
@@ -242,87 +177,31 @@ class ShardedAggregation:
             self.send_index[:n].copy_(sp_index_local)
         if self.stats:  # this rank's pair, all-gathered with its rows
             from .ops import cbsr_stats
-            cbsr_stats(self.send_data[:n], self.send_index[:n],
-                       out=self.stats_words(self.send_index, self.part.rows_per_phase))
-
-    @staticmethod
-    def stats_words(index_table: torch.Tensor, row: int) -> torch.Tensor:
-        """The 2 int32 statistics words in the selector bytes of a spare row."""
-        return index_table[row].view(torch.int32)[:2]
-
-    def _gather_phase(self, p: int, async_op: bool):
-        w1 = dist.all_gather_into_tensor(self._slice(self.table_data, p),
-                                         self._send_slice(self.send_data, p),
-                                         group=self.group, async_op=async_op)
-        w2 = dist.all_gather_into_tensor(self._slice(self.table_index, p),
-                                         self._send_slice(self.send_index, p),
-                                         group=self.group, async_op=async_op)
-        return (w1, w2)
+            cbsr_stats(self.send_data[:n], self.send_index[:n], out=self._stats_words_send)
 
     def gather(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> None:
-        """All-gather this rank's CBSR rows into the padded tables (RCCL over xGMI)."""
+        """All-gather this rank's CBSR records into the padded table (one RCCL collective)."""
         self._stage(sp_data_local, sp_index_local)
-        for p in range(self.part.phases):
-            self._gather_phase(p, async_op=False)
+        dist.all_gather_into_tensor(self.table_rec, self.send_rec, group=self.group)
 
     def forward(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> torch.Tensor:
-        self._stage(sp_data_local, sp_index_local)
-        P = self.part.phases
-        works = [self._gather_phase(p, async_op=True) for p in range(P)]
-        if self.split:
-            # own columns from the send buffers while the exchange is in flight
-            out = self._fwd(0, self.send_data[: self.n_local], self.send_index[: self.n_local],
-                            None)
-            for wk in works[0]:
-                wk.wait()
-            return self._fwd(1, self.table_data, self.table_index, out)
-        out = None
-        for p in range(P):
-            for wk in works[p]:
-                wk.wait()   # the compute stream waits for phase p only
-            out = self._fwd(p, self._slice(self.table_data, p), self._slice(self.table_index, p),
-                            out)
-        return out
+        self.gather(sp_data_local, sp_index_local)
+        return self._fwd(self.table_data, self.table_index)
 
     def compute_forward(self) -> torch.Tensor:
-        """The forward's kernels alone on the current tables (no exchange): per-rank timing."""
-        if self.split:
-            out = self._fwd(0, self.send_data[: self.n_local], self.send_index[: self.n_local],
-                            None)
-            return self._fwd(1, self.table_data, self.table_index, out)
-        out = None
-        for p in range(self.part.phases):
-            out = self._fwd(p, self._slice(self.table_data, p), self._slice(self.table_index, p),
-                            out)
-        return out
+        """The forward's kernels alone on the current table (no exchange): per-rank timing."""
+        return self._fwd(self.table_data, self.table_index)
 
     def backward(self, grad_out_local: torch.Tensor) -> torch.Tensor:
-        g = grad_out_local.contiguous()
-        if self.split:  # the all-edges plan, then the one-shot reduce-scatter
-            gp = self._bwd(2, g, self.table_index)
-            dist.reduce_scatter_tensor(self.grad_local, gp, op=dist.ReduceOp.SUM,
-                                       group=self.group)
-            return self.grad_local[: self.n_local]
-        works = []
-        for p in range(self.part.phases):
-            gp = self._bwd(p, g, self._slice(self.table_index, p))
-            works.append(dist.reduce_scatter_tensor(self._send_slice(self.grad_local, p), gp,
-                                                    op=dist.ReduceOp.SUM, group=self.group,
-                                                    async_op=True))
-        for wk in works:
-            wk.wait()
+        gp = self._bwd(grad_out_local.contiguous(), self.table_index)
+        dist.reduce_scatter_tensor(self.grad_local, gp, op=dist.ReduceOp.SUM, group=self.group)
         return self.grad_local[: self.n_local]
 
-    def compute_backward(self, grad_out_local: torch.Tensor) -> None:
+    def compute_backward(self, grad_out_local: torch.Tensor) -> torch.Tensor:
         """The backward's kernels alone (no exchange): per-rank timing."""
-        g = grad_out_local.contiguous()
-        if self.split:
-            self._bwd(2, g, self.table_index)
-            return
-        for p in range(self.part.phases):
-            self._bwd(p, g, self._slice(self.table_index, p))
+        return self._bwd(grad_out_local.contiguous(), self.table_index)
 
     def unpad_table(self, table: torch.Tensor) -> torch.Tensor:
-        """Padded phase-major table -> natural node order [N, ...] (tests/inspection)."""
+        """Padded table -> natural node order [N, ...] (tests/inspection)."""
         return torch.cat([table[self.part.table_positions(q, table.device)]
                           for q in range(self.part.world_size)])

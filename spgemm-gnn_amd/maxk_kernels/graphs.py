@@ -5,6 +5,10 @@ Generator: per-row in-degrees from a seeded log
 columns drawn uniformly without replacement (excluding the row itself) and sorted, plus
 one self-loop per row (DGL ``AddSelfLoop``: run/reddit.log:28 reports 114,848,857 edges
 after it). Seed 97 is the reference default (utils/config.py:54).
+
+:func:`synthetic_csr` draws the columns from torch's generator (the tests' graphs);
+:func:`synthetic_ptr` + :func:`synthetic_rows` (the bench graph since round 4) draw them from a
+counter-based stream, so each rank of a row partition generates only its own rows.
 """
 from __future__ import annotations
 
@@ -82,6 +86,80 @@ def synthetic_csr(num_nodes: int, num_edges: int, seed: int = 97, sigma: float =
     return ptr.to(torch.int32), cols.to(torch.int32)
 
 
+_M64 = (1 << 64) - 1
+
+
+def _i64(c: int) -> int:
+    """A 64-bit constant as the int64 value with the same bits (torch has no uint64 math)."""
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+def _srl(z: torch.Tensor, s: int) -> torch.Tensor:
+    """Logical right shift of int64 bit patterns."""
+    return (z >> s) & ((1 << (64 - s)) - 1)
+
+
+def hash_uniform(seed: int, index: torch.Tensor) -> torch.Tensor:
+    """Counter-based uniforms: splitmix64(seed * 2^32 + index) -> float64 in [0, 1) (53 bits).
+    Element i depends only on (seed, index[i]), so any slice of a stream (one rank's edges)
+    can be generated alone and equals that slice of the whole stream. int64 products wrap
+    modulo 2^64 as the unsigned arithmetic of splitmix64 does."""
+    z = index.to(torch.int64) + (int(seed) << 32) + _i64(0x9E3779B97F4A7C15)
+    z = (z ^ _srl(z, 30)) * _i64(0xBF58476D1CE4E5B9)
+    z = (z ^ _srl(z, 27)) * _i64(0x94D049BB133111EB)
+    z = z ^ _srl(z, 31)
+    return _srl(z, 11).to(torch.float64) * (2.0 ** -53)
+
+
+def synthetic_ptr(num_nodes: int, num_edges: int, seed: int = 97, sigma: float = 1.2,
+                  device="cpu") -> torch.Tensor:
+    """ptr (int32 [N+1]) of :func:`synthetic_rows`'s graph: lognormal degrees (the same
+    generator as :func:`synthetic_csr`) plus one self-loop per row. O(N): every rank of a
+    row partition computes it to balance its rows before generating only those."""
+    device = torch.device(device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    n = int(num_nodes)
+    deg = lognormal_degrees(n, int(num_edges) - n, sigma, gen, device) + 1
+    ptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    ptr[1:] = torch.cumsum(deg, 0)
+    return ptr.to(torch.int32)
+
+
+def synthetic_rows(ptr: torch.Tensor, seed: int = 97, rows=None) -> torch.Tensor:
+    """Column ids (int32, sorted per row) of rows [r0, r1) of the graph whose ptr is
+    :func:`synthetic_ptr`'s: row r holds its self-loop plus deg(r) - 1 columns drawn uniformly
+    without replacement from the other nodes, the draws of its edges coming from the
+    counter-based stream :func:`hash_uniform` at the edges' global positions. A rank that
+    generates only its rows gets exactly those rows of the whole graph (bench.py: every
+    world size benchmarks the same graph, and no rank builds the 115 M-edge whole).
+    Host syncs: one (the two edge offsets)."""
+    n = ptr.numel() - 1
+    r0, r1 = (0, n) if rows is None else (int(rows[0]), int(rows[1]))
+    dev = ptr.device
+    p = ptr[r0:r1 + 1].to(torch.int64)
+    e0, e1 = (int(x) for x in torch.stack([p[0], p[-1]]).tolist())
+    deg = p[1:] - p[:-1] - 1                          # draws per row (self-loop excluded)
+    m = e1 - e0 - (r1 - r0)
+    rl = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), deg, output_size=m)
+    row = rl + r0
+    # draw j of row r: uniform index in [0, n - 1 - deg(r)]; sorted, t_j = s_j + j is a sorted
+    # deg-subset of [0, n - 1); shifting t >= r by one excludes the row itself
+    start = torch.cumsum(deg, 0) - deg
+    gpos = (p[:-1] - (torch.arange(r1 - r0, device=dev) + r0))[rl] + (torch.arange(m, device=dev) - start[rl])
+    span = (n - 1 - deg)[rl] + 1
+    s = torch.floor(hash_uniform(seed, gpos) * span.to(torch.float64)).to(torch.int64)
+    s = torch.minimum(s, span - 1)
+    key, _ = torch.sort(rl * n + s)
+    s = key - rl * n
+    cols = s + (torch.arange(m, device=dev) - start[rl])
+    cols = cols + (cols >= row).to(torch.int64)
+    del key, s, span, gpos
+    ar = torch.arange(r1 - r0, device=dev)
+    key, _ = torch.sort(torch.cat([rl, ar]) * n + torch.cat([cols, ar + r0]))
+    return (key - (key // n) * n).to(torch.int32)
+
+
 def community_csr(num_nodes: int, num_edges: int, communities: int = 41, p_in: float = 0.76,
                   seed: int = 97, sigma: float = 1.2, shuffle: bool = False, device="cpu"):
     """A locality-bearing variant of :func:`synthetic_csr` (supplementary measurements only,
@@ -127,11 +205,13 @@ def row_degrees(ptr: torch.Tensor) -> torch.Tensor:
     return (ptr[1:] - ptr[:-1]).to(torch.int64)
 
 
-def sage_mean_values(ptr: torch.Tensor) -> torch.Tensor:
-    """val[nz] = 1/deg(row) (SAGE mean; utils/maxk_layers.py:147-157)."""
+def sage_mean_values(ptr: torch.Tensor, num_edges: Optional[int] = None) -> torch.Tensor:
+    """val[nz] = 1/deg(row) (SAGE mean; utils/maxk_layers.py:147-157). ``num_edges``
+    (= ptr[-1] - ptr[0], when the caller knows it) spares the host sync that
+    ``repeat_interleave`` otherwise makes to size its output."""
     deg = row_degrees(ptr)
     inv = 1.0 / deg.clamp(min=1).to(torch.float32)
-    return torch.repeat_interleave(inv, deg)
+    return torch.repeat_interleave(inv, deg, output_size=num_edges)
 
 
 def gcn_values(ptr: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:

@@ -25,7 +25,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import ACC_KINDS, COL_ORDERS, PlanInfo, PlanOptions, check, lib
+from ._lib import ACC_KINDS, BWD_ALGOS, COL_ORDERS, PlanInfo, PlanOptions, check, lib
 
 TOPK_MODES = {"exact": 0, "ref_compat": 1}
 
@@ -59,6 +59,17 @@ def _check_tensor(t: torch.Tensor, name: str, dtype: Optional[torch.dtype] = Non
         _need(t.dtype == dtype, f"{name} must be {str(dtype).replace('torch.', '')}")
 
 
+def _table(t: torch.Tensor, name: str, dtype: torch.dtype, rows: int, k: int) -> int:
+    """A [rows, k] CBSR table whose rows may be strided (interleaved records): returns the row
+    stride in elements."""
+    _need(isinstance(t, torch.Tensor) and t.is_cuda, f"{name} must be a CUDA tensor")
+    _need(t.dtype == dtype, f"{name} must be {str(dtype).replace('torch.', '')}")
+    _need(t.dim() == 2 and tuple(t.shape) == (rows, k), f"{name} must be [{rows}, {k}]")
+    _need(t.stride(1) == 1 and (rows <= 1 or t.stride(0) >= k),
+          f"{name} must have unit column stride and row stride >= k")
+    return t.stride(0) if rows > 1 else k
+
+
 # -------------------------------------------------------------------------------------
 # MaxK top-k
 # -------------------------------------------------------------------------------------
@@ -71,8 +82,9 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
     ``mode='exact'`` selects the true top-k (utils/models.py:14 semantics), ``'ref_compat'``
     the reference kernel's 8-step bisection, bit-exact. With ``return_index=True`` returns
     ``(sp_data, sp_index)`` with ``sp_index`` u8 ``[N, k]`` in ascending feature order.
-    ``out=(sp_data, sp_index)`` writes into caller-owned contiguous ``[N, k]`` tensors (e.g.
-    the send buffers of :class:`maxk_kernels.dist.ShardedAggregation`). ``return_count=True``
+    ``out=(sp_data, sp_index)`` writes into caller-owned ``[N, k]`` tables with unit column
+    stride (rows may be strided: the interleaved send records of
+    :class:`maxk_kernels.dist.ShardedAggregation`). ``return_count=True``
     appends the int32 ``[N]`` number of filled slots per row (``k`` in exact mode; in
     ref_compat mode the slots past it are the reference's ``(0.0f, 0)`` padding).
     """
@@ -87,18 +99,18 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
     if out is None:
         sp_data = torch.empty((n, k), dtype=torch.float32, device=input.device)
         sp_index = torch.empty((n, k), dtype=torch.uint8, device=input.device)
+        ds = is_ = k
     else:
         sp_data, sp_index = out
-        _need(sp_data.shape == (n, k) and sp_data.dtype == torch.float32 and
-              sp_data.is_contiguous() and sp_data.device == input.device,
-              "out[0] must be a contiguous float32 [N, k] tensor on the input's device")
-        _need(sp_index.shape == (n, k) and sp_index.dtype == torch.uint8 and
-              sp_index.is_contiguous() and sp_index.device == input.device,
-              "out[1] must be a contiguous uint8 [N, k] tensor on the input's device")
+        _need(sp_data.device == input.device and sp_index.device == input.device,
+              "out must be on the input's device")
+        ds = _table(sp_data, "out[0]", torch.float32, n, k)
+        is_ = _table(sp_index, "out[1]", torch.uint8, n, k)
     count = torch.empty(n, dtype=torch.int32, device=input.device) if return_count else None
     with _device(input.device):
-        check(lib.maxk_topk_cbsr_count(_p(input), _p(sp_data), _p(sp_index), _p(count), n, d,
-                                       k, TOPK_MODES[mode], _stream()), "maxk_forward")
+        check(lib.maxk_topk_cbsr_tables(_p(input), _p(sp_data), ds, _p(sp_index), is_,
+                                        _p(count), n, d, k, TOPK_MODES[mode], _stream()),
+              "maxk_forward")
     res = (sp_data, sp_index) if return_index else (sp_data,)
     if return_count:
         res = res + (count,)
@@ -155,9 +167,9 @@ class GraphPlan:
                  num_cols: Optional[int] = None, options: Optional[dict] = None,
                  col_order: Optional[torch.Tensor] = None):
         """``options``: ``maxk_plan_options`` fields by name (``col_order`` also by name:
-        'identity', 'scattered', 'clustered'); ``col_order``: an int32 device permutation of
-        the columns (position -> column) for the backward's column blocks, which selects
-        ``col_order='given'``."""
+        'identity', 'scattered'; ``bwd_algo``: 'column_blocks', 'two_pass'); ``col_order``: an
+        int32 device permutation of the columns (position -> column) for the backward's
+        column blocks, which selects ``col_order='given'``."""
         self.handle = ctypes.c_void_p(0)
         self.device = ptr.device
         self._refs = (ptr, idx, val)  # keep the graph's storage alive while cached
@@ -174,6 +186,8 @@ class GraphPlan:
                 value = ACC_KINDS[value]
             if key == "col_order" and isinstance(value, str):
                 value = COL_ORDERS[value]
+            if key == "bwd_algo" and isinstance(value, str):
+                value = BWD_ALGOS[value]
             setattr(opts, key, int(value))
         if col_order is not None:
             _check_tensor(col_order, "col_order", torch.int32)
@@ -213,8 +227,8 @@ class GraphPlan:
             return torch.empty(nbytes, dtype=torch.uint8, device=self.device), nbytes
         except torch.OutOfMemoryError:
             # the two-pass backward's product workspace is the large one (one row chunk of
-            # E x k x 4 bytes, <= 4 GiB by default): give the allocator its cached blocks
-            # back once, then say which knob bounds it
+            # E x k x 4 bytes, <= 16 GiB by default, kBwdTwoPassWorkspaceCap): give the
+            # allocator its cached blocks back once, then say which knob bounds it
             torch.cuda.empty_cache()
             try:
                 return torch.empty(nbytes, dtype=torch.uint8, device=self.device), nbytes
@@ -226,7 +240,8 @@ class GraphPlan:
 
     def forward(self, sp_data, sp_index, out=None, accumulate: bool = False,
                 stats=None) -> torch.Tensor:
-        """SpGEMM with this plan: sp tables [num_cols, k] -> out [num_rows, D];
+        """SpGEMM with this plan: sp tables [num_cols, k] (rows may be strided, e.g. the
+        interleaved records of :mod:`maxk_kernels.dist`, gathered in place) -> out [num_rows, D];
         ``accumulate=True`` adds into the given ``out`` instead of overwriting it. ``stats``:
         fixed-point statistics covering the table instead of a pass over it, either an int32
         [n, 2] tensor of :func:`cbsr_stats` pairs or ``(tensor, n, stride)`` with pair i at
@@ -251,11 +266,13 @@ class GraphPlan:
                   stats.dim() == 2 and stats.shape[1] == 2 and stats.shape[0] >= 1,
                   "stats must be a contiguous int32 [n, 2] CUDA tensor")
             st, n_st = stats, stats.shape[0]
-        check(lib.maxk_spgemm_forward_ex(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
-                                         _p(sp_index), _p(out), self.num_rows, self.num_edges,
-                                         self.dim_k, self.dim_origin, int(accumulate), _p(st),
-                                         n_st, stride, _p(ws), wsb,
-                                         ctypes.c_void_p(stream.cuda_stream)),
+        ds = _table(sp_data, "sp_data", torch.float32, self.num_cols, self.dim_k)
+        is_ = _table(sp_index, "sp_index", torch.uint8, self.num_cols, self.dim_k)
+        check(lib.maxk_spgemm_forward_tables(self.handle, _p(ptr), _p(idx), _p(val), _p(sp_data),
+                                             ds, _p(sp_index), is_, _p(out), self.num_rows,
+                                             self.num_edges, self.dim_k, self.dim_origin,
+                                             int(accumulate), _p(st), n_st, stride, _p(ws), wsb,
+                                             ctypes.c_void_p(stream.cuda_stream)),
               "spgemm_forward")
         self._end(stream)
         return out
@@ -269,10 +286,12 @@ class GraphPlan:
         stream = torch.cuda.current_stream(self.device)
         self._begin(stream)
         ws, wsb = self._workspace(self.bwd_ws_bytes)
-        check(lib.maxk_sspmm_backward_ws(self.handle, _p(ptr), _p(idx), _p(val), _p(grad_out),
-                                         _p(sp_index), _p(grad_sp), self.num_rows,
-                                         self.num_edges, self.dim_k, self.dim_origin, _p(ws),
-                                         wsb, ctypes.c_void_p(stream.cuda_stream)),
+        is_ = _table(sp_index, "sp_index", torch.uint8, self.num_cols, self.dim_k)
+        check(lib.maxk_sspmm_backward_tables(self.handle, _p(ptr), _p(idx), _p(val),
+                                             _p(grad_out), _p(sp_index), is_, _p(grad_sp),
+                                             self.num_rows, self.num_edges, self.dim_k,
+                                             self.dim_origin, _p(ws), wsb,
+                                             ctypes.c_void_p(stream.cuda_stream)),
               "spgemm_backward")
         self._end(stream)
         return grad_sp
@@ -448,17 +467,18 @@ def cbsr_stats(sp_data: torch.Tensor, sp_index: torch.Tensor,
                out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fixed-point statistics of a CBSR table (``maxk_cbsr_stats``): int32 [1, 2] (written
     into ``out`` when given), the pair :meth:`GraphPlan.forward` takes as ``stats``."""
-    _check_tensor(sp_data, "sp_data", torch.float32)
-    _check_tensor(sp_index, "sp_index", torch.uint8)
     _need(sp_data.dim() == 2 and sp_index.shape == sp_data.shape,
           "sp_data and sp_index must be [N, k]")
+    n, k = sp_data.shape
+    ds = _table(sp_data, "sp_data", torch.float32, n, k)
+    is_ = _table(sp_index, "sp_index", torch.uint8, n, k)
     if out is None:
         out = torch.empty((1, 2), dtype=torch.int32, device=sp_data.device)
     _need(out.is_cuda and out.is_contiguous() and out.dtype == torch.int32 and out.numel() == 2,
           "out must be a contiguous int32 CUDA tensor of 2 elements")
     with torch.cuda.device(sp_data.device):
-        check(lib.maxk_cbsr_stats(_p(sp_data), _p(sp_index), sp_data.shape[0], sp_data.shape[1],
-                                  _p(out), _stream()), "cbsr_stats")
+        check(lib.maxk_cbsr_stats_tables(_p(sp_data), ds, _p(sp_index), is_, n, k, _p(out),
+                                         _stream()), "cbsr_stats")
     return out
 
 

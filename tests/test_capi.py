@@ -25,7 +25,7 @@ def declared_functions():
 def test_library_is_in_tree_and_loaded():
     assert os.path.exists(_lib.LIB_PATH)
     assert _lib.LIB_PATH.startswith(os.path.join(ROOT, "spgemm-gnn_amd"))
-    assert maxk_kernels.ABI_VERSION == 2
+    assert maxk_kernels.ABI_VERSION == 3
 
 
 def test_exports_every_declared_symbol():
@@ -229,8 +229,10 @@ def test_plan_create_sized_option_sizes():
     assert lib.maxk_plan_create_sized(*args, ctypes.cast(bigger, ctypes.c_void_p), size + 8,
                                       None, None, ctypes.byref(h)) == -1
     assert "null pointer" in lib.maxk_last_error().decode()   # ... then ptr = NULL is refused
-    # the version-1 layout is 120 bytes (round-1 options, up to fwd_rot_rate)
+    # the version-1 layout is 144 bytes (up to bwd_tp_store; the round-1 layout ended at
+    # fwd_rot_rate, 120 bytes)
     assert _lib.PlanOptions.bwd_flush.offset == 31 * 4 and _lib.PlanOptions.external_workspace.offset == 120
+    assert _lib.PlanOptions.bwd_row_cost.offset == 144
     # an ABI-2 option (col_order = 4) needs the permutation argument
     opts.col_order = 4
     assert lib.maxk_plan_create_sized(*args, ctypes.byref(opts), size, None, None,
@@ -239,3 +241,37 @@ def test_plan_create_sized_option_sizes():
     assert not h.value
     info = _lib.PlanInfo()
     assert lib.maxk_plan_get_info_sized(None, ctypes.byref(info), ctypes.sizeof(info)) == -1
+
+
+def _header_enum(prefix):
+    text = open(HEADER).read()
+    return {m.group(1): int(m.group(2))
+            for m in re.finditer(r"\b(" + prefix + r"\w+)\s*=\s*(-?\d+)", text)}
+
+
+def test_header_enums_match_binding():
+    """The documented enumerations the library writes into maxk_plan_info (col_order, bwd_algo)
+    and reads from the options equal the Python binding's name tables."""
+    co = _header_enum("MAXK_COL_ORDER_")
+    assert {k.replace("MAXK_COL_ORDER_", "").lower(): v for k, v in co.items()} == _lib.COL_ORDERS
+    ba = _header_enum("MAXK_BWD_")
+    assert {k.replace("MAXK_BWD_", "").lower(): v for k, v in ba.items()} == _lib.BWD_ALGOS
+    v1 = int(re.search(r"#define MAXK_PLAN_OPTIONS_V1_BYTES (\d+)", open(HEADER).read()).group(1))
+    assert v1 == _lib.PlanOptions.bwd_row_cost.offset == 144
+
+
+def test_removed_options_refused_on_host():
+    """ABI 3: option values of removed kernel organisations are refused before any device
+    call, with MAXK_ERR_UNSUPPORTED and a message naming the option."""
+    lib = _lib.lib
+    h = ctypes.c_void_p(0)
+    for name, value in (("col_order", 3), ("bwd_algo", 2), ("fwd_persistent", 1),
+                        ("bwd_features_per_lane", 1), ("quad_loads", 2)):
+        opts = _lib.PlanOptions()
+        setattr(opts, name, value)
+        rc = lib.maxk_plan_create_sized(None, None, None, 10, 10, 100, 256, 16, ctypes.byref(opts),
+                                        ctypes.sizeof(opts), None, None, ctypes.byref(h))
+        assert rc == -2, name
+        msg = lib.maxk_last_error().decode()
+        assert "removed in ABI 3" in msg and name.split("_")[0] in msg, msg
+    assert not h.value

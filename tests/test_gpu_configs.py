@@ -129,35 +129,42 @@ def _sampled_cols_ok(gs, ptr, idx, val, sp_index, g, ncols=400, seed=1):
 
 @pytest.mark.parametrize("k", [16])
 def test_config5_reddit_w8_partition(gpu, k):
+    """BASELINE config 5 emulated on one GPU: the bench graph (each rank generates only its
+    rows), every rank's ShardedAggregation over the all-gathered record table (filled here as
+    the one RCCL all-gather would, statistics pairs included), the reduce-scatter as a sum."""
+    from maxk_kernels.dist import ShardedAggregation, record_bytes, record_views
     D, W = 256, 8
     n, e = graphs.DATASETS["reddit"]
-    ptr, idx = graphs.synthetic_csr(n, e, seed=97, device=gpu)
-    val = graphs.sage_mean_values(ptr)
+    ptr = graphs.synthetic_ptr(n, e, seed=97, device=gpu)
     h = graphs.features(n, D, seed=97, device=gpu)
     g = graphs.features(n, D, seed=98, device=gpu)
     sp_data, sp_index = mk.maxk_forward(h, k, return_index=True)
     del h
     part = RowPartition(ptr, W)
-    assert part.phases == 1 and part.padded_rows >= n
-    # the padded all-gather tables every rank holds after the forward exchange
-    table_d = torch.zeros((part.padded_rows, k), device=gpu)
-    table_i = torch.zeros((part.padded_rows, k), dtype=torch.uint8, device=gpu)
+    assert part.padded_rows >= n
+    # the padded record table every rank holds after the forward exchange
+    table_rec = torch.zeros((part.padded_rows, record_bytes(k)), dtype=torch.uint8, device=gpu)
+    td, ti = record_views(table_rec, k)
     for q in range(W):
         a, b = part.rows(q)
         pos = part.table_positions(q, gpu)
-        table_d[pos] = sp_data[a:b]
-        table_i[pos] = sp_index[a:b]
+        td[pos] = sp_data[a:b]
+        ti[pos] = sp_index[a:b]
+        mk.cbsr_stats(sp_data[a:b], sp_index[a:b],
+                      out=table_rec.view(torch.int32)[part.stats_position(q), :2])
     y = torch.empty((n, D), device=gpu)
     grad_table = torch.zeros((part.padded_rows, k), device=gpu)
     ranks_e = []
     for q in range(W):
         a, b = part.rows(q)
-        lp, li, lv = part.local_csr(ptr, idx, val, q)
-        ranks_e.append(li.numel())
-        plan = mk.GraphPlan(lp, li, lv, b - a, li.numel(), D, k, num_cols=part.phase_cols)
-        y[a:b] = plan.forward(table_d, table_i)
-        grad_table += plan.backward(g[a:b].contiguous(), table_i)     # the reduce-scatter
-        del plan
+        idx_q = graphs.synthetic_rows(ptr, seed=97, rows=(a, b))
+        val_q = graphs.sage_mean_values(ptr[a:b + 1], num_edges=idx_q.numel())
+        ranks_e.append(idx_q.numel())
+        shard = ShardedAggregation(part, q, ptr, idx_q, val_q, D, k, local_edges=True)
+        shard.table_rec.copy_(table_rec)
+        y[a:b] = shard.compute_forward()
+        grad_table += shard.compute_backward(g[a:b])                    # the reduce-scatter
+        del shard
     torch.cuda.synchronize()
     gs = torch.cat([grad_table[part.table_positions(q, gpu)] for q in range(W)])
     # nnz balance of the partition (SURVEY §8(e)): every rank within 1 % of E / W
@@ -168,6 +175,8 @@ def test_config5_reddit_w8_partition(gpu, k):
     scale = (y.double().abs() * g.double().abs()).sum().item()
     assert abs(lhs - rhs) <= 1e-5 * scale
     # the single-GPU plan on the whole graph gives the same sums
+    idx = graphs.synthetic_rows(ptr, seed=97)
+    val = graphs.sage_mean_values(ptr, num_edges=e)
     y1, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, n, e, k, D)
     g1 = mk.spgemm_backward(ptr, idx, val, g, sp_index, n, e, k, D)
     assert ((y - y1).abs() <= 2e-5 * y1.abs().max()).all()

@@ -1,8 +1,9 @@
 """GPU: the row-partitioned path of maxk_kernels.dist on one device.
 
-* emulated W-rank partition: each rank's rectangular plan (columns remapped into the padded
-  all-gather table) run on the GPU, the all-gather / reduce-scatter done with tensor ops;
-  the union of the ranks' outputs must match the oracle on the whole graph;
+* emulated W-rank partition: each rank's ShardedAggregation (a rectangular plan over the
+  padded table of interleaved CBSR records) run on the GPU, the all-gather / reduce-scatter
+  done with tensor ops; the union of the ranks' outputs must match the oracle on the whole
+  graph; records gathered in place give bitwise the output of the contiguous tables;
 * ShardedAggregation end to end over a real RCCL ("nccl") process group of world size 1.
 """
 import os
@@ -26,64 +27,28 @@ def _graph(n=6000, e=150_000, seed=41):
     return p, i, graphs.sage_mean_values(p)
 
 
-@pytest.mark.parametrize("world,phases,opts", [(2, 1, None), (3, 1, None), (8, 1, None),
-                                               (2, 2, None), (8, 2, None), (3, 3, None),
-                                               (2, 1, {"bwd_algo": 3}), (8, 2, {"bwd_algo": 3})])
-@pytest.mark.parametrize("k", [16, 32])
-def test_emulated_partition_matches_oracle(gpu, world, phases, opts, k):
-    """Every rank's per-phase rectangular plans (columns remapped into the phase-major
-    padded table) on one GPU; the all-gather / reduce-scatter done with tensor ops; also
-    with the two-pass backward forced on every shard."""
-    p, i, v = _graph()
-    n, d = p.numel() - 1, 256
-    x = graphs.features(n, d, seed=5)
-    g = graphs.features(n, d, seed=6)
-    od, oi = oracle.maxk(x.numpy(), k)
-    ref_f, mag_f = oracle.spgemm_forward(p.numpy(), i.numpy(), v.numpy(), od, oi, d, with_mag=True)
-    ref_b, mag_b = oracle.sspmm_backward(p.numpy(), i.numpy(), v.numpy(), g.numpy(), oi,
-                                         with_mag=True)
-    ptr, idx, val = p.to(gpu), i.to(gpu), v.to(gpu)
-    part = RowPartition(ptr, world, phases=phases)
-    # the padded all-gather table every rank would hold
-    table_d = torch.zeros((part.padded_rows, k), device=gpu)
-    table_i = torch.zeros((part.padded_rows, k), dtype=torch.uint8, device=gpu)
-    for q in range(world):
-        a, b = part.rows(q)
-        pos = part.table_positions(q, gpu)
-        table_d[pos] = torch.from_numpy(od[a:b]).to(gpu)
-        table_i[pos] = torch.from_numpy(oi[a:b]).to(gpu)
-    y = torch.empty((n, d), device=gpu)
-    grad_table = torch.zeros((part.padded_rows, k), device=gpu)
-    nc = part.phase_cols
-    for q in range(world):
-        a, b = part.rows(q)
-        lp, li, lv = part.local_csr(ptr, idx, val, q)
-        out = torch.empty((b - a, d), device=gpu)
-        for ph in range(phases):
-            pp, pi, pv = part.phase_csr(lp, li, lv, ph)
-            plan = mk.GraphPlan(pp, pi, pv, b - a, pi.numel(), d, k, num_cols=nc, options=opts)
-            if opts and pi.numel() > 0:
-                assert plan.info()["bwd_algo"] == 3
-            plan.forward(table_d[ph * nc:(ph + 1) * nc], table_i[ph * nc:(ph + 1) * nc], out,
-                         accumulate=ph > 0)
-            grad_table[ph * nc:(ph + 1) * nc] += plan.backward(                # reduce-scatter
-                g[a:b].contiguous().to(gpu), table_i[ph * nc:(ph + 1) * nc])
-        y[a:b] = out
-    gs = torch.cat([grad_table[part.table_positions(q, gpu)] for q in range(world)])
-    ok, worst = oracle.close_enough(y.cpu().numpy(), ref_f, mag_f)
-    assert ok, worst
-    # per-rank partials summed in f32 (the reduce-scatter): the same bar
-    ok, worst = oracle.close_enough(gs.cpu().numpy(), ref_b, mag_b)
-    assert ok, worst
+def _fill_tables(part, sd, si, shard, gpu):
+    """The all-gather emulated: every rank's rows and statistics pair in the shard's table."""
+    world = part.world_size
+    for r in range(world):
+        ra, rb = part.rows(r)
+        pos = part.table_positions(r, gpu)
+        shard.table_data[pos] = sd[ra:rb]
+        shard.table_index[pos] = si[ra:rb]
+        sp = part.stats_position(r)
+        mk.cbsr_stats(sd[ra:rb], si[ra:rb], out=shard.table_rec.view(torch.int32)[sp, :2])
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-@pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("k", [16, 32])
-def test_emulated_shards_stats_and_split(gpu, world, split, k):
-    """ShardedAggregation as every rank builds it (statistics row in each rank's block; the
-    local-columns-first split), the all-gather emulated by filling each rank's table and
-    statistics rows, the reduce-scatter by summing the ranks' partial gradients."""
+@pytest.mark.parametrize("world,opts", [(2, None), (3, None), (8, None), (2, {"bwd_algo": 3}),
+                                        (8, {"bwd_algo": 3}), (4, {"fwd_two_tables": 1}),
+                                        (4, {"fwd_two_tables": 2}), (8, {"fwd_fixed": 2})])
+@pytest.mark.parametrize("k", [8, 16, 32, 12])
+def test_emulated_shards_match_oracle(gpu, world, opts, k):
+    """ShardedAggregation as every rank builds it (one rectangular plan over the interleaved
+    record table, a statistics pair in each rank's spare record), the all-gather emulated by
+    filling each rank's table, the reduce-scatter by summing the ranks' partial gradients; the
+    union of the ranks' outputs against the oracle on the whole graph. The forward gathers the
+    records in place (no per-call pack) whatever table layout the plan would pick."""
     p, i, v = _graph()
     n, d = p.numel() - 1, 256
     od, oi = oracle.maxk(graphs.features(n, d, seed=15).numpy(), k)
@@ -97,32 +62,63 @@ def test_emulated_shards_stats_and_split(gpu, world, split, k):
     y = torch.empty((n, d), device=gpu)
     grad_sum = torch.zeros((part.padded_rows, k), device=gpu)
     for q in range(world):
-        shard = ShardedAggregation(part, q, ptr, idx, val, d, k, split=split)
-        assert shard.stats and len(shard.plans) == (3 if split else 1)
+        e0, e1 = part.edges(ptr, q)
+        shard = ShardedAggregation(part, q, ptr, idx[e0:e1].clone(), val[e0:e1].clone(), d, k,
+                                   plan_options=opts, local_edges=True)
+        assert shard.stats
         a, b = part.rows(q)
-        shard._stage(sd[a:b], si[a:b])
-        for r in range(world):
-            ra, rb = part.rows(r)
-            pos = part.table_positions(r, gpu)
-            shard.table_data[pos] = sd[ra:rb]
-            shard.table_index[pos] = si[ra:rb]
-            sp = part.stats_position(r)
-            shard.table_data[sp] = 0.0
-            shard.table_index[sp] = 0
-            mk.cbsr_stats(sd[ra:rb], si[ra:rb], out=shard.stats_words(shard.table_index, sp))
-        # the rank's own statistics row went out with its send buffer; its values stay zero
-        assert torch.equal(shard.send_index[part.rows_per_phase],
-                           shard.table_index[part.stats_position(q)])
-        assert not shard.send_data[part.rows_per_phase].any()
+        bd, bi = shard.local_buffers()
+        mk.maxk_forward(graphs.features(n, d, seed=15)[a:b].contiguous().to(gpu), k,
+                        out=(bd, bi))                       # top-k into the send records
+        assert torch.equal(bd, sd[a:b]) and torch.equal(bi, si[a:b])
+        shard._stage(bd, bi)
+        _fill_tables(part, sd, si, shard, gpu)
+        # the rank's own statistics pair went out with its send records
+        assert torch.equal(shard.send_rec[part.max_rows, :8],
+                           shard.table_rec[part.stats_position(q), :8])
         y[a:b] = shard.compute_forward()
-        gl = gg[a:b].contiguous()
-        grad_sum += shard._bwd(2 if split else 0, gl, shard.table_index)
+        grad_sum += shard.compute_backward(gg[a:b])
         del shard
     gs = torch.cat([grad_sum[part.table_positions(q, gpu)] for q in range(world)])
     ok, worst = oracle.close_enough(y.cpu().numpy(), ref_f, mag_f)
     assert ok, worst
+    # per-rank partials summed in f32 (the reduce-scatter): the same bar
     ok, worst = oracle.close_enough(gs.cpu().numpy(), ref_b, mag_b)
     assert ok, worst
+
+
+@pytest.mark.parametrize("k", [16, 32])
+def test_records_in_place_equal_packed(gpu, k):
+    """The forward over interleaved records (gathered in place) gives bitwise the output of the
+    same plan over the two contiguous tables (packed per call or gathered as two tables), and
+    the backward reading selectors at the record stride meets the oracle bar like the one
+    reading sp_index (both backward algorithms)."""
+    from maxk_kernels.dist import record_bytes, record_views
+    p, i, v = _graph(n=5000, e=200_000, seed=44)
+    n, d = p.numel() - 1, 256
+    ptr, idx, val = p.to(gpu), i.to(gpu), v.to(gpu)
+    x = graphs.features(n, d, seed=17).to(gpu)
+    g = graphs.features(n, d, seed=18).to(gpu)
+    sd, si = mk.maxk_forward(x, k, return_index=True)
+    rec = torch.zeros((n, record_bytes(k)), dtype=torch.uint8, device=gpu)
+    rd, ri = record_views(rec, k)
+    mk.maxk_forward(x, k, out=(rd, ri))
+    assert torch.equal(rd, sd) and torch.equal(ri, si)
+    ref_b, mag_b = oracle.sspmm_backward(p.numpy(), i.numpy(), v.numpy(), g.cpu().numpy(),
+                                         si.cpu().numpy(), with_mag=True)
+    for opts in ({}, {"fwd_two_tables": 1}, {"fwd_two_tables": 2}, {"fwd_fixed": 2},
+                 {"bwd_algo": 3}):
+        plan = mk.GraphPlan(ptr, idx, val, n, i.numel(), d, k, options=opts)
+        a = plan.forward(sd, si)
+        b = plan.forward(rd, ri)
+        torch.cuda.synchronize()
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), opts
+        # (the column blocks' float CAS order varies from call to call: the oracle bar)
+        for sel in (si, ri):
+            ok, worst = oracle.close_enough(plan.backward(g, sel).cpu().numpy(), ref_b, mag_b)
+            assert ok, (opts, worst)
+    st = mk.cbsr_stats(rd, ri)
+    assert torch.equal(st, mk.cbsr_stats(sd, si))
 
 
 def test_forward_accumulate_vs_oracle(gpu):
@@ -152,9 +148,8 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("phases,opts,split", [(1, None, False), (2, None, False),
-                                               (1, {"bwd_algo": 3}, False), (1, None, True)])
-def test_sharded_aggregation_rccl_world1(gpu, phases, opts, split):
+@pytest.mark.parametrize("opts", [None, {"bwd_algo": 3}])
+def test_sharded_aggregation_rccl_world1(gpu, opts):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
@@ -165,8 +160,8 @@ def test_sharded_aggregation_rccl_world1(gpu, phases, opts, split):
         x = graphs.features(n, d, seed=7).to(gpu)
         g = graphs.features(n, d, seed=8).to(gpu)
         sd, si = mk.maxk_forward(x, k, return_index=True)
-        part = RowPartition(ptr, 1, phases=phases)
-        shard = ShardedAggregation(part, 0, ptr, idx, val, d, k, plan_options=opts, split=split)
+        part = RowPartition(ptr, 1)
+        shard = ShardedAggregation(part, 0, ptr, idx, val, d, k, plan_options=opts)
         y = shard.forward(sd, si)
         gs = shard.backward(g)
         od, oi = sd.cpu().numpy(), si.cpu().numpy()
@@ -179,7 +174,7 @@ def test_sharded_aggregation_rccl_world1(gpu, phases, opts, split):
         assert ok, worst
         ok, worst = oracle.close_enough(gs.cpu().numpy(), g_ref, g_mag)
         assert ok, worst
-        # top-k written straight into the send buffers (bench.py's N > 1 step): no copies
+        # top-k written straight into the send records (bench.py's N > 1 step): no copies
         sdb, sib = shard.local_buffers()
         r = mk.maxk_forward(x, k, return_index=True, out=(sdb, sib))
         assert r[0] is sdb and r[1] is sib

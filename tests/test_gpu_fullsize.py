@@ -136,6 +136,73 @@ def test_every_row_and_column_vs_oracle(case):
     print(f"backward: worst err/bound {_close_in_chunks(gs.cpu().numpy(), ref, mag):.3g}")
 
 
+def test_config3_autograd_step_vs_oracle(gpu):
+    """BASELINE config 3 as its training step runs it: ogbn-products (full size), SAGE-mean
+    values, D = 256, k = 32, through the autograd surface (MaxKFunction -> SpGEMMFunction,
+    which picks the two-pass backward here). Every element of the output and of the input
+    gradient against the oracle's composition maxk_backward(SSpMM(G)) (f64 sums)."""
+    _GRAPHS.clear()
+    _FEATS.clear()
+    mk.clear_plan_cache()
+    torch.cuda.empty_cache()
+    n, e = graphs.DATASETS["ogbn-products"]
+    k = 32
+    ptr, idx = graphs.synthetic_csr(n, e, seed=97, device=gpu)
+    val = graphs.sage_mean_values(ptr)
+    h = graphs.features(n, D, seed=97, device=gpu).requires_grad_(True)
+    g = graphs.features(n, D, seed=98, device=gpu)
+    graph = mk.CSRGraph(ptr, idx, val)
+    sp_data, sp_index = mk.maxk(h, k)
+    y = mk.spgemm(sp_data, sp_index, graph, D)
+    y.backward(g)
+    torch.cuda.synchronize()
+    assert mk.get_plan(ptr, idx, val, n, e, D, k).info()["bwd_algo"] == 3
+    p, ix, v = ptr.cpu().numpy(), idx.cpu().numpy(), val.cpu().numpy()
+    od, oi = oracle.maxk(h.detach().cpu().numpy(), k)
+    assert np.array_equal(sp_index.cpu().numpy(), oi)
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, D, with_mag=True)
+    print(f"forward: worst err/bound {_close_in_chunks(y.detach().cpu().numpy(), ref, mag):.3g}")
+    del y, ref, mag
+    gs, gmag = oracle.sspmm_backward(p, ix, v, g.cpu().numpy(), oi, with_mag=True)
+    gx_ref = oracle.maxk_backward(gs, oi, D)
+    gx_mag = oracle.maxk_backward(gmag, oi, D)
+    del gs, gmag
+    print(f"input gradient: worst err/bound "
+          f"{_close_in_chunks(h.grad.cpu().numpy(), gx_ref, gx_mag):.3g}")
+    mk.clear_plan_cache()
+
+
+@pytest.mark.parametrize("algo", [1, 3])
+def test_backward_grad_out_beyond_4gib(gpu, algo):
+    """grad_out larger than 4 GiB (N * D * 4 > 2^32: the column-block records then hold row
+    indices and the gathers are 64-bit addressed instead of 32-bit buffer offsets), both
+    backward algorithms, every output element against the oracle."""
+    _GRAPHS.clear()
+    _FEATS.clear()
+    mk.clear_plan_cache()
+    torch.cuda.empty_cache()
+    n, e, k = 4_300_000, 9_000_000, 16
+    ptr, idx = graphs.synthetic_csr(n, e, seed=91, device=gpu)
+    val = graphs.sage_mean_values(ptr)
+    assert n * D * 4 > 2 ** 32
+    gen = torch.Generator(device=gpu)
+    gen.manual_seed(92)
+    g = torch.randn(n, D, generator=gen, device=gpu)
+    si = torch.argsort(torch.rand(n, D, generator=gen, device=gpu), dim=1)[:, :k]
+    si = torch.sort(si, dim=1).values.to(torch.uint8).contiguous()
+    plan = mk.GraphPlan(ptr, idx, val, n, idx.numel(), D, k, options=dict(bwd_algo=algo))
+    assert plan.info()["bwd_algo"] == algo
+    gs = plan.backward(g, si)
+    torch.cuda.synchronize()
+    ref, mag = oracle.sspmm_backward(ptr.cpu().numpy(), idx.cpu().numpy(), val.cpu().numpy(),
+                                     g.cpu().numpy(), si.cpu().numpy(), with_mag=True)
+    print(f"backward (algo {algo}): worst err/bound "
+          f"{_close_in_chunks(gs.cpu().numpy(), ref, mag):.3g}")
+    del plan, gs, g
+    mk.clear_plan_cache()
+    torch.cuda.empty_cache()
+
+
 # ------------------------------------------------------------------ top-k at config size
 # north_star: "bit-exact on the top-k index output". Every BASELINE case's feature matrix
 # (N(0,1), seed 97, D=256) through maxk_forward in both modes against oracle.maxk: indices

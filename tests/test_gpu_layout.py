@@ -1,8 +1,9 @@
 """GPU: the ABI-2 layout options against the oracle.
 
-* column orders of the backward's column blocks (identity / scattered / clustered / the
-  caller's permutation) and the chunk bounds (equal edges / equal cost), on graphs with and
-  without community structure in ID order;
+* column orders of the backward's column blocks (identity / scattered / the caller's
+  permutation, checked through the raw C ABI against the header's documented values) and the
+  row order of the block streams, on graphs with and without community structure in ID
+  order;
 * row chunks of the two-pass backward (bounded workspace);
 * the fixed-point forward's bound with repeated selectors (maxk_hip.h: repeated selectors in
   one CBSR row are summed) and the per-part statistics of maxk_spgemm_forward_ex;
@@ -53,11 +54,10 @@ def dev(a, gpu):
 
 
 @pytest.mark.parametrize("gname", ["uniform", "community", "community_shuffled"])
-@pytest.mark.parametrize("order", ["identity", "scattered", "clustered"])
-@pytest.mark.parametrize("bounds", [2, 3])
+@pytest.mark.parametrize("order", ["identity", "scattered", "given"])
 @pytest.mark.parametrize("k", [8, 16, 32])
 @pytest.mark.parametrize("rows", [1, 2])
-def test_col_order_and_chunk_bounds_vs_oracle(gpu, gname, order, bounds, k, rows):
+def test_col_order_and_row_order_vs_oracle(gpu, gname, order, k, rows):
     p, ix, v = graph(gname)
     n, d = p.size - 1, 256
     x = graphs.features(n, d, seed=k)
@@ -65,14 +65,20 @@ def test_col_order_and_chunk_bounds_vs_oracle(gpu, gname, order, bounds, k, rows
     od, oi = oracle.maxk(x.numpy(), k)
     ref_f, mag_f = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
     ref_b, mag_b = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
-    plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k,
-                        options=dict(col_order=order, bwd_chunk_bounds=bounds,
-                                     bwd_row_order=rows, bwd_tasks_per_cu=8,
-                                     bwd_min_task_edges=2000))
+    opts = dict(bwd_row_order=rows, bwd_tasks_per_cu=8, bwd_min_task_edges=2000)
+    perm = None
+    if order == "given":
+        perm = torch.from_numpy(np.random.RandomState(k).permutation(n).astype(np.int32)).to(gpu)
+    else:
+        opts["col_order"] = order
+    plan = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k, options=opts,
+                        col_order=perm)
     info = plan.info()
     assert info["bwd_row_order"] == rows
-    assert info["col_order"] == {"identity": 1, "scattered": 2, "clustered": 3}[order]
-    assert info["bwd_chunk_bounds"] == bounds
+    assert info["col_order"] == _lib.COL_ORDERS[order]
+    assert info["bwd_chunk_bounds"] == 2
+    if perm is not None:
+        assert torch.equal(mk.plan_col_order(plan), perm)
     assert_close(plan.forward(dev(od, gpu), dev(oi, gpu)), ref_f, mag_f)
     gs = plan.backward(g.to(gpu), dev(oi, gpu))
     assert_close(gs, ref_b, mag_b)
@@ -82,6 +88,58 @@ def test_col_order_and_chunk_bounds_vs_oracle(gpu, gname, order, bounds, k, rows
     torch.cuda.synchronize()
     assert not torch.isnan(again).any()
     assert_close(again, ref_b, mag_b)
+
+
+def _header_enum(prefix):
+    import os
+    import re
+    text = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             "include", "maxk_hip.h")).read()
+    return {m.group(1): int(m.group(2))
+            for m in re.finditer(r"\b(" + prefix + r"\w+)\s*=\s*(\d+)", text)}
+
+
+@pytest.mark.parametrize("mode", ["MAXK_COL_ORDER_AUTO", "MAXK_COL_ORDER_IDENTITY",
+                                  "MAXK_COL_ORDER_SCATTERED", "MAXK_COL_ORDER_GIVEN"])
+def test_capi_col_order_info_matches_header(gpu, mode):
+    """maxk_plan_create_sized with each documented col_order value, straight through the C
+    ABI: maxk_plan_info.col_order reads back the header's enumeration (auto = identity), and
+    maxk_plan_get_col_order returns the order the blocks use."""
+    enum = _header_enum("MAXK_COL_ORDER_")
+    p, ix, v = graph("uniform")
+    n, d, k = p.size - 1, 256, 16
+    dp, di, dv = dev(p, gpu), dev(ix, gpu), dev(v, gpu)
+    opts = _lib.PlanOptions()
+    opts.col_order = enum[mode]
+    perm = torch.from_numpy(np.random.RandomState(3).permutation(n).astype(np.int32)).to(gpu)
+    h = ctypes.c_void_p(0)
+    P = ctypes.c_void_p
+    rc = _lib.lib.maxk_plan_create_sized(P(dp.data_ptr()), P(di.data_ptr()), P(dv.data_ptr()),
+                                         n, n, ix.size, d, k, ctypes.byref(opts),
+                                         ctypes.sizeof(opts),
+                                         P(perm.data_ptr()) if mode.endswith("GIVEN") else None,
+                                         P(torch.cuda.current_stream().cuda_stream),
+                                         ctypes.byref(h))
+    assert rc == 0, _lib.lib.maxk_last_error()
+    try:
+        info = _lib.PlanInfo()
+        assert _lib.lib.maxk_plan_get_info_sized(h, ctypes.byref(info), ctypes.sizeof(info)) == 0
+        want = enum["MAXK_COL_ORDER_IDENTITY"] if mode.endswith("AUTO") else enum[mode]
+        assert info.col_order == want
+        assert info.bwd_algo == _header_enum("MAXK_BWD_")["MAXK_BWD_COLUMN_BLOCKS"]
+        got = torch.empty(n, dtype=torch.int32, device=gpu)
+        assert _lib.lib.maxk_plan_get_col_order(h, P(got.data_ptr()),
+                                                P(torch.cuda.current_stream().cuda_stream)) == 0
+        torch.cuda.synchronize()
+        if mode.endswith("GIVEN"):
+            assert torch.equal(got, perm)
+        elif mode.endswith("SCATTERED"):
+            assert torch.equal(torch.sort(got.long()).values, torch.arange(n, device=gpu))
+            assert not torch.equal(got.long(), torch.arange(n, device=gpu))
+        else:
+            assert torch.equal(got.long(), torch.arange(n, device=gpu))
+    finally:
+        _lib.lib.maxk_plan_destroy(h)
 
 
 def test_given_col_order(gpu):
@@ -97,46 +155,16 @@ def test_given_col_order(gpu):
     assert_close(plan.backward(g.to(gpu), dev(oi, gpu)), ref, mag)
     got = mk.plan_col_order(plan)
     assert torch.equal(got, perm)
-    bad = perm.clone()
-    bad[7] = bad[8]                        # not a permutation
-    with pytest.raises(RuntimeError, match="permutation"):
-        mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k, col_order=bad)
-    bad[7] = n                             # out of range
-    with pytest.raises(RuntimeError, match="permutation"):
-        mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k, col_order=bad)
-
-
-def test_clustered_order_recovers_hidden_communities(gpu):
-    """On a community graph under a random relabelling, the clustered order puts each
-    community's columns at neighbouring positions: every column block is mostly one
-    community (the scattered and identity orders mix all of them)."""
-    n, e, c = 30_000, 3_000_000, 9
-    ptr, idx = graphs.community_csr(n, e, communities=c, seed=73, shuffle=True, device=gpu)
-    # community of each relabelled node: replay the generator's permutation
-    gen = torch.Generator(device=gpu)
-    gen.manual_seed(73)
-    deg = graphs.lognormal_degrees(n, e - n, 1.2, gen, gpu)
-    m = int(deg.sum())
-    torch.rand(m, generator=gen, device=gpu, dtype=torch.float64)
-    torch.rand(m, generator=gen, device=gpu)
-    perm = torch.randperm(n, generator=gen, device=gpu)
-    size = -(-n // c)
-    comm = torch.empty(n, dtype=torch.int64, device=gpu)
-    comm[perm] = torch.arange(n, device=gpu) // size
-    val = graphs.sage_mean_values(ptr)
-    purity = {}
-    for order in ("identity", "clustered"):
-        plan = mk.GraphPlan(ptr, idx, val, n, idx.numel(), 256, 16, options=dict(col_order=order))
-        C = plan.info()["bwd_block_cols"]
-        pos = mk.plan_col_order(plan) if order == "clustered" else torch.arange(n, device=gpu)
-        labels = comm[pos.long()]
-        pur = []
-        for b0 in range(0, n, C):
-            lab = labels[b0:b0 + C]
-            pur.append(torch.bincount(lab, minlength=c).max().item() / lab.numel())
-        purity[order] = float(np.mean(pur))
-    assert purity["identity"] < 0.3
-    assert purity["clustered"] > 0.8, purity
+    # not a permutation: a repeat, and entries outside [0, n) far beyond the buffer (refused
+    # on the host before any device scatter uses them)
+    for bad_value in ("repeat", n, -1, 1 << 30, -(1 << 30)):
+        bad = perm.clone()
+        bad[7] = bad[8] if bad_value == "repeat" else bad_value
+        with pytest.raises(RuntimeError, match="permutation"):
+            mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k, col_order=bad)
+    # the device is still healthy and the good order still works
+    again = mk.GraphPlan(dev(p, gpu), dev(ix, gpu), dev(v, gpu), n, ix.size, d, k, col_order=perm)
+    assert_close(again.backward(g.to(gpu), dev(oi, gpu)), ref, mag)
 
 
 @pytest.mark.parametrize("chunks", [1, 2, 7])

@@ -170,6 +170,36 @@ def test_offset_views_through_every_entry_point(gpu, k):
     assert_close(y, ref, mag, rtol=2e-6 * 64)  # f32 sums in two orders (test_dense_spmm_vs_oracle)
 
 
+@pytest.mark.parametrize("levels", [4, 16, 256])
+@pytest.mark.parametrize("k", [8, 16, 32, 64])
+def test_topk_ties_vs_torch_topk(gpu, levels, k):
+    """Tie-heavy rows (features quantised to a few levels): the exact mode's selection against
+    torch.topk on the same device, the top-k the reference trained with (utils/models.py:14,
+    ``x.topk(k, dim=1)``). Both must select the same multiset of values; where a tie at the
+    k-th value lets them pick different indices, ours is the lowest-index choice (the oracle's
+    rule, bit-exact), and the share of such rows is reported."""
+    n, d = 20_000, 256
+    x = graphs.features(n, d, seed=levels + k)
+    x = torch.round(x * (levels / 8.0)) / (levels / 8.0)     # ~levels distinct values per row
+    xg = x.to(gpu)
+    sd, si = mk.maxk_forward(xg, k, mode="exact", return_index=True)
+    tv, ti = torch.topk(xg, k, dim=1)
+    # same selected values (as a multiset) per row
+    assert torch.equal(torch.sort(sd, dim=1).values, torch.sort(tv, dim=1).values)
+    ours = torch.zeros_like(xg, dtype=torch.bool).scatter_(1, si.long(), True)
+    theirs = torch.zeros_like(xg, dtype=torch.bool).scatter_(1, ti, True)
+    differ = (ours != theirs).any(dim=1)
+    # ours: bit-exact with the lowest-index rule
+    od, oi = oracle.maxk(x.numpy(), k)
+    assert np.array_equal(si.cpu().numpy(), oi)
+    # where the sets differ, the k-th value is tied across the boundary
+    kth = tv[:, -1:]
+    on_tie = ((ours ^ theirs) & ~(xg == kth)).any(dim=1)
+    assert not on_tie.any()
+    print(f"ties: levels={levels} k={k}: torch.topk picked other indices on "
+          f"{int(differ.sum())} of {n} rows ({100.0 * differ.float().mean().item():.2f} %)")
+
+
 def test_topk_default_returns_reference_shape(gpu):
     x = graphs.features(10, 64, seed=1).to(gpu)
     out = mk.maxk_forward(x, 16)
@@ -371,7 +401,7 @@ def test_sspmm_backward_golden(gpu, golden, k):
 
 @pytest.mark.parametrize("gname", list(GRAPHS))
 @pytest.mark.parametrize("d,k", [(256, 8), (256, 16), (256, 32), (256, 64), (256, 24),
-                                 (64, 16), (100, 10), (128, 70), (256, 256)])
+                                 (64, 16), (100, 10), (128, 70), (256, 256), (256, 5), (256, 250)])
 def test_sspmm_backward_vs_oracle(gpu, gname, d, k):
     p, ix, v = GRAPHS[gname]()
     n = p.size - 1
@@ -402,22 +432,27 @@ def test_sspmm_backward_two_slots_vs_oracle(gpu, gname, k):
 
 
 @pytest.mark.parametrize("gname", list(GRAPHS))
-@pytest.mark.parametrize("k", [4, 8, 16, 32, 64, 24])
-@pytest.mark.parametrize("feats", [4, 1])
-def test_sspmm_backward_csc_vs_oracle(gpu, gname, k, feats):
-    """Column-major backward (bwd_algo=2); k=24 (6 lanes per edge) falls back to the blocks."""
+@pytest.mark.parametrize("d,k", [(256, 1), (256, 3), (256, 7), (256, 13), (64, 17), (256, 61),
+                                 (256, 130), (256, 199), (256, 255)])
+@pytest.mark.parametrize("feats", [0, 4, 2])
+def test_sspmm_backward_padded_slots_vs_oracle(gpu, gname, d, k, feats):
+    """k that is not a multiple of the slots per lane F: the column-block kernel pads the
+    selector slots to a multiple of F (padding slots gather feature 0 into accumulators
+    that are never stored), with the default F, four and two slots per lane; every element of
+    grad_sp is written, and value refreshes reach the records."""
     p, ix, v = GRAPHS[gname]()
-    n, d = p.size - 1, 256
+    n = p.size - 1
     x = graphs.features(n, d, seed=k)
     g = graphs.features(n, d, seed=k + 1)
     _, oi = oracle.maxk(x.numpy(), k)
     ref, mag = oracle.sspmm_backward(p, ix, v, g.numpy(), oi, with_mag=True)
     ptr, idx, val = graph_on(gpu, p, ix, v)
-    plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k,
-                        options=dict(bwd_algo=2, bwd_features_per_lane=feats))
-    assert plan.info()["bwd_algo"] == (1 if k == 24 or ix.size == 0 else 2)
-    assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
-    val.mul_(-2.0)                        # refresh_values rewrites the column-major records
+    opts = dict(bwd_algo=1) if feats == 0 else dict(bwd_algo=1, bwd_features_per_lane=feats)
+    plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k, options=opts)
+    gs = torch.full((n, k), float("nan"), device=gpu)
+    plan.backward(g.to(gpu), to_dev(oi, gpu), gs)
+    assert_close(gs, ref, mag)
+    val.mul_(-2.0)                        # refresh_values rewrites the records' values
     ref, mag = oracle.sspmm_backward(p, ix, v * -2.0, g.numpy(), oi, with_mag=True)
     plan.refresh_values(val)
     assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
@@ -465,7 +500,7 @@ def test_sspmm_backward_auto_twopass_on_sparse_wide_graph(gpu):
     assert_close(forced.backward(g.to(gpu), to_dev(oi, gpu)), ref, mag)
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("algo", [0, 1, 3])
 @pytest.mark.parametrize("k", [16, 32])
 def test_unsorted_rows_and_multi_edges(gpu, algo, k):
     """CSR rows with shuffled column order and repeated (row, column) edges: every edge
@@ -565,90 +600,71 @@ def test_dense_spmm_vs_oracle(gpu):
 # every maxk_plan_options knob the C ABI exposes selects a different kernel organisation;
 # each must give the same results (the defaults are covered above)
 PLAN_OPTIONS = [
-    dict(fwd_tile_rows=16), dict(fwd_tile_rows=1), dict(fwd_tile_rows=64),
-    dict(fwd_accumulator="f32_cas"), dict(fwd_tile_rows=64, fwd_accumulator="f32_cas"),
-    dict(fwd_phases=3), dict(fwd_persistent=1), dict(fwd_unroll=16), dict(fwd_task_cap=512),
-    dict(fwd_rotate=2), dict(fwd_persistent=1, fwd_rotate=2),
-    dict(bwd_accumulator="f64"), dict(bwd_features_per_lane=1), dict(bwd_order=1),
-    dict(bwd_unroll=16), dict(bwd_slot_groups=2), dict(bwd_slot_groups=4),
-    dict(bwd_lds_bytes=4096), dict(bwd_tasks_per_cu=1), dict(bwd_acc_pad=2), dict(bwd_sel_lds=2),
-    dict(bwd_unroll=4), dict(bwd_unroll=12),
-    dict(bwd_algo=2), dict(bwd_algo=2, bwd_unroll=4), dict(bwd_algo=3),
-    dict(bwd_algo=2, bwd_features_per_lane=1), dict(bwd_algo=2, bwd_features_per_lane=1, bwd_unroll=16),
+    dict(fwd_tile_rows=16), dict(fwd_tile_rows=1), dict(fwd_tile_rows=64), dict(fwd_task_cap=512),
+    dict(fwd_rotate=2), dict(fwd_rot_windows=64), dict(fwd_rot_windows=3, fwd_rot_rate=1),
+    dict(bwd_unroll=12), dict(bwd_unroll=16), dict(bwd_waves=12), dict(bwd_waves=12, bwd_unroll=16),
+    dict(bwd_slot_groups=2), dict(bwd_slot_groups=4), dict(bwd_lds_bytes=4096),
+    dict(bwd_tasks_per_cu=1), dict(bwd_algo=3), dict(bwd_algo="two_pass"),
+    # the accepted spellings of the defaults of removed knobs
+    dict(fwd_accumulator="f64", bwd_accumulator="f32_cas", fwd_unroll=8, fwd_waves=4,
+         bwd_acc_pad=2, bwd_sel_lds=1, fwd_prefetch=2, bwd_prefetch=2, fwd_branchless=1,
+         bwd_cas64=1, bwd_tp_store=1, bwd_chunk_bounds=2, fwd_phases=1),
     # chunked blocks (slab flush by default, atomic flush into a memset grad_sp with
-    # bwd_flush=1; bwd_order=1 always flushes atomically), both task orders
+    # bwd_flush=1)
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=1),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=2, external_workspace=1),
-    dict(bwd_tasks_per_cu=64, bwd_min_task_edges=16, bwd_features_per_lane=1),
+    dict(bwd_tasks_per_cu=64, bwd_min_task_edges=16, bwd_features_per_lane=2),
     # pieces: every (block, chunk) task cut into pieces of <= 500 edges (slab regions per
-    # piece), with chunks, slot groups, the one-slot kernel and the atomic flush
+    # piece), with chunks, slot groups, two slots per lane and the atomic flush
     dict(bwd_piece_edges=500), dict(bwd_piece_edges=500, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(bwd_piece_edges=500, bwd_slot_groups=2), dict(bwd_piece_edges=500, bwd_features_per_lane=1),
+    dict(bwd_piece_edges=500, bwd_slot_groups=2), dict(bwd_piece_edges=500, bwd_features_per_lane=2),
     dict(bwd_piece_edges=500, bwd_flush=1),
-    # two slots per lane (k/2 lanes per edge): unrolls, slot groups, dword CAS, chunks
-    dict(bwd_features_per_lane=2), dict(bwd_features_per_lane=2, bwd_unroll=12),
+    # two slots per lane (k/2 lanes per edge): unrolls, slot groups, chunks, more waves
+    dict(bwd_features_per_lane=2), dict(bwd_features_per_lane=2, bwd_unroll=8),
     dict(bwd_features_per_lane=2, bwd_unroll=16), dict(bwd_features_per_lane=2, bwd_slot_groups=2),
-    dict(bwd_features_per_lane=2, bwd_cas64=2), dict(bwd_features_per_lane=2, quad_loads=2),
+    dict(bwd_features_per_lane=2, bwd_waves=12),
     dict(bwd_features_per_lane=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    # chunk bounds shared by every block (the per-block equal-edge bounds are the default)
-    dict(bwd_chunk_bounds=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(bwd_chunk_bounds=1, bwd_piece_edges=500),
-    dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_order=1),
     dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_slot_groups=2),
-    dict(bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_accumulator="f64"),
-    # wavefronts per work-group, edge-stream prefetch, branchless idle lanes, record stride
-    dict(fwd_waves=6), dict(fwd_waves=8, fwd_prefetch=1), dict(fwd_prefetch=1),
-    dict(fwd_branchless=1), dict(fwd_branchless=2), dict(fwd_record_bytes=256),
-    dict(bwd_waves=12), dict(bwd_waves=16), dict(bwd_prefetch=1),
-    dict(bwd_waves=12, bwd_prefetch=1), dict(bwd_waves=16, bwd_prefetch=1),
     dict(bwd_waves=12, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    # lane-chunk forward records; one-slot-per-lane packed backward
-    dict(fwd_chunk3=1), dict(fwd_chunk3=2), dict(fwd_chunk3=1, fwd_record_bytes=256),
-    dict(fwd_chunk3=1, fwd_waves=8, fwd_prefetch=1), dict(fwd_chunk3=1, fwd_branchless=2),
-    dict(bwd_features_per_lane=1, bwd_unroll=16), dict(bwd_features_per_lane=1, bwd_waves=12),
-    dict(bwd_features_per_lane=1, bwd_waves=16),
-    dict(bwd_features_per_lane=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    # dword CAS (the 64-bit CAS pairs are the default), padded pair layout, with chunks
-    dict(bwd_cas64=2), dict(bwd_acc_pad=1), dict(bwd_unroll=12), dict(bwd_unroll=16),
-    dict(bwd_cas64=2, bwd_waves=12), dict(bwd_cas64=2, bwd_prefetch=1),
-    dict(bwd_slot_groups=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_acc_pad=1),
-    # quad-shared record loads: off, forward too, with prefetch / more waves / unroll 12
-    dict(quad_loads=2), dict(quad_loads=1), dict(quad_loads=1, fwd_prefetch=1),
-    dict(quad_loads=1, fwd_chunk3=1), dict(bwd_prefetch=1, bwd_waves=16),
-    dict(fwd_two_tables=1), dict(fwd_two_tables=2), dict(fwd_two_tables=1, fwd_prefetch=1),
-    dict(fwd_rot_windows=64), dict(fwd_rot_windows=3, fwd_rot_rate=1),
-    # forward accumulation: f64 atomics only; fixed point with the other forward layouts
-    dict(fwd_fixed=2), dict(fwd_fixed=2, fwd_two_tables=1), dict(fwd_fixed=1, fwd_chunk3=1),
-    dict(fwd_fixed=1, fwd_unroll=16), dict(fwd_fixed=1, fwd_tile_rows=64),
-    dict(fwd_fixed=1, quad_loads=1), dict(fwd_fixed=1, fwd_phases=3),
-    # two-pass backward with the products stored in column order
-    dict(bwd_algo=3, bwd_tp_store=2), dict(bwd_algo=3, bwd_tp_store=1),
-    # ABI 2: chunk bounds (equal edges / equal cost with two pair costs), column orders of
-    # the backward blocks (scattered, clustered) with every packed kernel and flush, two-pass
-    # row chunks
-    dict(bwd_chunk_bounds=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(bwd_chunk_bounds=3, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(bwd_chunk_bounds=3, bwd_row_cost=400, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(bwd_chunk_bounds=3, bwd_row_cost=1, bwd_tasks_per_cu=64, bwd_min_task_edges=16),
-    dict(col_order="scattered"), dict(col_order="clustered"),
+    # lane-chunk forward records, two tables, fixed point / f64 with each forward layout
+    dict(fwd_chunk3=1), dict(fwd_chunk3=2), dict(fwd_chunk3=1, fwd_fixed=2),
+    dict(fwd_two_tables=1), dict(fwd_two_tables=2), dict(fwd_two_tables=1, fwd_fixed=2),
+    dict(fwd_fixed=2), dict(fwd_fixed=1, fwd_chunk3=1), dict(fwd_fixed=1, fwd_tile_rows=64),
+    dict(fwd_fixed=1, fwd_two_tables=1), dict(fwd_fixed=1, fwd_rotate=2),
+    # column orders of the backward blocks (scattered, identity) with chunks, pieces, the
+    # two-slot kernel, slot groups and the two-pass (which ignores them)
+    dict(col_order="scattered"), dict(col_order="identity"),
     dict(col_order="scattered", bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(col_order="clustered", bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=1),
-    dict(col_order="scattered", bwd_features_per_lane=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(col_order="scattered", bwd_tasks_per_cu=32, bwd_min_task_edges=256, bwd_flush=1),
     dict(col_order="scattered", bwd_features_per_lane=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(col_order="clustered", bwd_slot_groups=2, bwd_piece_edges=500),
-    dict(col_order="clustered", bwd_lds_bytes=4096), dict(col_order="scattered", bwd_sel_lds=2),
-    dict(col_order="scattered", bwd_algo=3), dict(col_order="clustered", bwd_algo=2),
-    dict(col_order="clustered", bwd_accumulator="f64"),
-    dict(col_order="identity", bwd_chunk_bounds=1, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
+    dict(col_order="scattered", bwd_slot_groups=2, bwd_piece_edges=500),
+    dict(col_order="scattered", bwd_lds_bytes=4096), dict(col_order="scattered", bwd_algo=3),
+    # two-pass row chunks
     dict(bwd_algo=3, bwd_tp_chunks=2), dict(bwd_algo=3, bwd_tp_chunks=5),
-    dict(bwd_algo=3, bwd_tp_chunks=3, bwd_tp_store=2),
-    # row order inside the block streams (ascending / scattered) with chunks, cost bounds,
-    # slot groups and a column order
+    # row order inside the block streams (ascending / scattered) with chunks, pieces, slot
+    # groups and a column order
     dict(bwd_row_order=1), dict(bwd_row_order=2, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(bwd_row_order=1, bwd_chunk_bounds=3, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
-    dict(bwd_row_order=2, col_order="clustered", bwd_slot_groups=2, bwd_piece_edges=500),
-    dict(bwd_row_order=2, bwd_features_per_lane=1, bwd_tasks_per_cu=64, bwd_min_task_edges=16),
+    dict(bwd_row_order=2, col_order="scattered", bwd_slot_groups=2, bwd_piece_edges=500),
+    dict(bwd_row_order=2, bwd_features_per_lane=2, bwd_tasks_per_cu=64, bwd_min_task_edges=16),
+]
+
+# option values refused with MAXK_ERR_UNSUPPORTED since ABI 3 (measured slower everywhere,
+# never auto-selected) and values that were never valid
+REMOVED_OPTIONS = [
+    dict(fwd_accumulator="f32_cas"), dict(bwd_accumulator="f64"), dict(bwd_features_per_lane=1),
+    dict(fwd_phases=3), dict(fwd_persistent=1), dict(fwd_unroll=16), dict(bwd_order=1),
+    dict(bwd_acc_pad=1), dict(bwd_sel_lds=2), dict(bwd_algo=2), dict(fwd_waves=8),
+    dict(fwd_prefetch=1), dict(bwd_prefetch=1), dict(fwd_record_bytes=256), dict(fwd_branchless=2),
+    dict(bwd_cas64=2), dict(quad_loads=1), dict(quad_loads=2), dict(bwd_chunk_bounds=1),
+    dict(bwd_chunk_bounds=3), dict(bwd_tp_store=2), dict(bwd_row_cost=8), dict(col_order=3),
+]
+INVALID_OPTIONS = [
+    dict(bwd_unroll=7), dict(bwd_unroll=4), dict(bwd_slot_groups=3), dict(fwd_tile_rows=65),
+    dict(bwd_lds_bytes=1 << 20), dict(bwd_algo=4), dict(bwd_waves=16), dict(fwd_chunk3=3),
+    dict(fwd_two_tables=3), dict(bwd_flush=3), dict(bwd_piece_edges=-1), dict(bwd_chunk_bounds=4),
+    dict(col_order=5), dict(col_order=4), dict(bwd_tp_chunks=-2), dict(bwd_row_order=3),
+    dict(bwd_features_per_lane=3), dict(fwd_fixed=3), dict(external_workspace=2),
 ]
 
 
@@ -668,7 +684,7 @@ def test_plan_options_vs_oracle(gpu, opts, k):
     assert_close(plan.backward(g.to(gpu), to_dev(oi, gpu)), ref_b, mag_b)
 
 
-@pytest.mark.parametrize("fpl", [4, 1])
+@pytest.mark.parametrize("fpl", [4, 2])
 def test_slab_flush_reproducible(gpu, fpl):
     """Chunked column blocks with the slab flush: the combine adds the chunk partials in
     chunk order, so two calls agree bitwise (the atomic flush only to the oracle bar), and
@@ -692,19 +708,15 @@ def test_slab_flush_reproducible(gpu, fpl):
     assert_close(a, ref_b, mag_b)
 
 
-def test_plan_options_rejected(gpu):
+@pytest.mark.parametrize("bad", REMOVED_OPTIONS + INVALID_OPTIONS,
+                         ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_plan_options_rejected(gpu, bad):
     p, ix, v = GRAPHS["single_node"]()
     ptr, idx, val = graph_on(gpu, p, ix, v)
-    for bad in (dict(fwd_unroll=7), dict(bwd_order=3), dict(bwd_slot_groups=3),
-                dict(fwd_tile_rows=65), dict(bwd_lds_bytes=1 << 20), dict(bwd_acc_pad=3),
-                dict(bwd_algo=4), dict(fwd_waves=5), dict(bwd_waves=10), dict(fwd_prefetch=3),
-                dict(fwd_record_bytes=72), dict(fwd_record_bytes=48), dict(fwd_branchless=3),
-                dict(fwd_chunk3=3), dict(fwd_chunk3=1, fwd_record_bytes=80), dict(bwd_cas64=3), dict(quad_loads=3), dict(fwd_two_tables=3),
-                dict(bwd_flush=3), dict(bwd_piece_edges=-1), dict(bwd_chunk_bounds=4),
-                dict(bwd_row_cost=-1), dict(col_order=5), dict(col_order=4),
-                dict(bwd_tp_chunks=-2), dict(bwd_row_order=3)):
-        with pytest.raises(RuntimeError):
-            mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
+    with pytest.raises(RuntimeError) as exc:
+        mk.GraphPlan(ptr, idx, val, 1, 1, 256, 16, options=bad)
+    if bad in REMOVED_OPTIONS:
+        assert "removed in ABI 3" in str(exc.value) and "code -2" in str(exc.value)
 
 
 # ------------------------------------------------------------------------ rocSPARSE comparator

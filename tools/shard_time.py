@@ -1,13 +1,14 @@
 """Per-rank device time of the row-partitioned path on ONE GPU (tooling): for W in 1,2,4,8
-build ranks' ShardedAggregation exactly as maxk_kernels.dist does, fill their gathered
-tables (and statistics rows) as the all-gather would, and time the forward and backward
-kernels alone (compute_forward / compute_backward: no collectives), to see how the compute
-part strong-scales and what the variants cost:
+build ranks' ShardedAggregation exactly as bench.py does (each rank generates its rows of the
+bench graph), fill their gathered record tables (and statistics pairs) as the one all-gather
+would, and time the forward and backward kernels alone (compute_forward / compute_backward: no
+collectives), to see how the compute part strong-scales:
 
-  stats   : the forward reads the W gathered statistics pairs (default) / scans the table
-  split   : the local-columns-first split (two plans per rank) / one plan
+  records : the forward gathers the all-gathered interleaved records in place (default);
+            "tables": the same plan over two contiguous tables (round 3's exchange layout,
+            packed per call or gathered as two tables)
 
-  python tools/shard_time.py [--k 16] [--worlds 1,2,4,8] [--variants '[...]']
+  python tools/shard_time.py [--k 16] [--worlds 1,2,4,8] [--opts '{}'] [--layouts records,tables]
 """
 import argparse
 import json
@@ -43,54 +44,48 @@ def main():
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--dataset", default="reddit")
     ap.add_argument("--worlds", default="1,2,4,8")
-    ap.add_argument("--variants", default='[{"split": false, "stats": true}, '
-                                          '{"split": false, "stats": false}, '
-                                          '{"split": true, "stats": true}]')
     ap.add_argument("--opts", default="{}", help="plan options (JSON dict)")
-    ap.add_argument("--phases", default="1", help="column phases to try (comma list; > 1 "
-                    "drops the statistics row)")
+    ap.add_argument("--layouts", default="records,tables")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS[args.dataset]
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
-    val = graphs.sage_mean_values(ptr)
+    ptr = graphs.synthetic_ptr(n, e, seed=97, device=dev)
     d, k = 256, args.k
     h = graphs.features(n, d, seed=97, device=dev)
     g = graphs.features(n, d, seed=98, device=dev)
     sd, si = mk.maxk_forward(h, k, return_index=True)
     del h
     opts = json.loads(args.opts)
-    for world, phases in [(int(w), int(p)) for w in args.worlds.split(",")
-                          for p in args.phases.split(",")]:
-        part = RowPartition(ptr, world, phases=phases)
-        for var in json.loads(args.variants):
+    for world in [int(w) for w in args.worlds.split(",")]:
+        part = RowPartition(ptr, world)
+        for layout in args.layouts.split(","):
             worst = 0.0
             for q in sorted({0, world - 1}):
-                shard = ShardedAggregation(part, q, ptr, idx, val, d, k, plan_options=opts,
-                                           split=var["split"])
                 a, b = part.rows(q)
-                shard._stage(sd[a:b], si[a:b])          # send buffers + this rank's stats row
-                shard.table_data.zero_()                # spare rows: zeros, as gathered
-                shard.table_index.zero_()
+                idx_q = graphs.synthetic_rows(ptr, seed=97, rows=(a, b))
+                val_q = graphs.sage_mean_values(ptr[a:b + 1], num_edges=idx_q.numel())
+                shard = ShardedAggregation(part, q, ptr, idx_q, val_q, d, k, plan_options=opts,
+                                           local_edges=True)
+                shard._stage(sd[a:b], si[a:b])          # send records + this rank's stats pair
                 for r in range(world):                  # the all-gather, emulated
                     ra, rb = part.rows(r)
                     pos = part.table_positions(r, dev)
                     shard.table_data[pos] = sd[ra:rb]
                     shard.table_index[pos] = si[ra:rb]
-                    if shard.stats:
-                        mk.cbsr_stats(sd[ra:rb], si[ra:rb],
-                                      out=shard.stats_words(shard.table_index,
-                                                            part.stats_position(r)))
-                shard.stats = shard.stats and var["stats"]
+                    mk.cbsr_stats(sd[ra:rb], si[ra:rb], out=shard.table_rec.view(
+                        torch.int32)[part.stats_position(r), :2])
+                td, ti = shard.table_data, shard.table_index
+                if layout == "tables":                  # two contiguous tables instead
+                    td, ti = td.contiguous(), ti.contiguous()
                 gl = g[a:b].contiguous()
-                tf = timeit(shard.compute_forward)
-                tb = timeit(lambda: shard.compute_backward(gl))
+                tf = timeit(lambda: shard.plan.forward(td, ti, stats=shard._stats_all))
+                tb = timeit(lambda: shard.plan.backward(gl, ti, shard.grad_table))
                 worst = max(worst, tf + tb)
-                print(json.dumps({"world": world, "phases": phases, **var, "opts": opts, "rank": q,
+                print(json.dumps({"world": world, "layout": layout, "opts": opts, "rank": q,
                                   "edges": int(shard.ptr[-1]), "fwd_ms": tf, "bwd_ms": tb,
-                                  "plans": [p.info() for p in shard.plans]}), flush=True)
+                                  "plan": shard.plan.info()}), flush=True)
                 del shard
-            print(json.dumps({"world": world, "phases": phases, **var, "opts": opts,
+            print(json.dumps({"world": world, "layout": layout, "opts": opts,
                               "compute_ms_max": worst,
                               "edges_per_s_compute_only": 2 * e / (worst * 1e-3)}), flush=True)
 
