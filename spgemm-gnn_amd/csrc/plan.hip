@@ -527,7 +527,8 @@ static int check_options(const maxk_plan_options& o) {
   MAXK_CHECK_ARG(o.bwd_unroll == 0 || o.bwd_unroll == 8 || o.bwd_unroll == 12 ||
                      o.bwd_unroll == 16,
                  "maxk_plan_create: bwd_unroll must be 0, 8, 12 or 16");
-  MAXK_CHECK_REMOVED(o.bwd_order == 0, "bwd_order = 1 (heavy-first tasks)");
+  MAXK_CHECK_REMOVED(o.bwd_order != 1, "bwd_order = 1 (heavy-first tasks)");
+  MAXK_CHECK_ARG(o.bwd_order >= 0 && o.bwd_order <= 2, "maxk_plan_create: bwd_order must be 0 or 2");
   MAXK_CHECK_ARG(o.bwd_slot_groups >= 0 && o.bwd_slot_groups <= 64 &&
                      (o.bwd_slot_groups & (o.bwd_slot_groups - 1)) == 0,
                  "maxk_plan_create: bwd_slot_groups must be 0 or a power of two <= 64");
@@ -1269,6 +1270,21 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       PLAN_TRY(hipStreamSynchronize(s));
       p->device_bytes += sizeof(int4) * comb.size();
     }
+  }
+  if (o.bwd_order == 2 && btasks.size() >= 2 * (size_t)kXcds) {
+    // XCD row windows: work-group i runs on XCD i % 8, one task per CU at a time. Within each
+    // round of `cus` consecutive (row-sorted) tasks, XCD x gets the x-th contiguous run of
+    // them, so the work-groups sharing an XCD's L2 sweep one row window of G instead of every
+    // window the round spans
+    const size_t R = (size_t)cus;
+    std::vector<BwdTask> dealt(btasks.size());
+    for (size_t r0 = 0; r0 < btasks.size(); r0 += R) {
+      const size_t n = std::min(R, btasks.size() - r0);
+      const size_t per = n / kXcds;
+      for (size_t q = 0; q < n; ++q)
+        dealt[r0 + q] = (n % kXcds == 0) ? btasks[r0 + (q % kXcds) * per + q / kXcds] : btasks[r0 + q];
+    }
+    btasks.swap(dealt);
   }
   p->n_bwd_tasks = (int32_t)btasks.size();
   p->n_bwd_shared = nshared;

@@ -851,38 +851,8 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
       T + (size_t)(e0 - ebase) * k, (short)0, (int)((uint32_t)(e1 - e0) * (uint32_t)k * 4u),
       0x00020000);
-  for (int base = e0; base < e1; base += EPS * U) {
-    uint32_t c[U];
-    float v[U];
-    if ((U & 3) == 0 && (L & 3) == 0) {
-      // lane q of a quad loads the record of sub-step 4j + q (contiguous), DPP hands it on:
-      // one record instruction per four sub-steps
-      const int qq = lane & 3;
-#pragma unroll
-      for (int j = 0; j < U / 4; ++j) {
-        const uint2 w2 = *reinterpret_cast<const uint2*>(
-            erec + 2 * (size_t)min(base + (4 * j + qq) * EPS + slot, e1 - 1));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int u = 4 * j + i;
-          if (u >= U) break;
-          c[u] = quad_pick(w2.x, i);
-          v[u] = __uint_as_float(quad_pick(w2.y, i));
-        }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = min(base + u * EPS + slot, e1 - 1);
-        const uint2 cv = *reinterpret_cast<const uint2*>(erec + 2 * (size_t)e);
-        c[u] = cv.x;  // column | (row % R) << kFwdColBits
-        v[u] = __uint_as_float(cv.y);
-      }
-    }
-    uint32_t sw[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      sw[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)(c[u] & kFwdColMask) * is + 4 * q);
+  auto compute_store = [&](int base, const uint32_t (&c)[U], const float (&v)[U],
+                           const uint32_t (&sw)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = base + u * EPS + slot;
@@ -897,6 +867,72 @@ __global__ __launch_bounds__(256) void sspmm_bwd_rows_kernel(
       // 5.58 -> 5.35 ms for both passes, ogbn-products k = 32 8.71 -> 8.56)
       __builtin_amdgcn_raw_buffer_store_b128(o, tr, off, 0, 2);
     }
+  };
+  auto load_sel = [&](const uint32_t (&c)[U], uint32_t (&sw)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      sw[u] = *reinterpret_cast<const uint32_t*>(sp_index + (size_t)(c[u] & kFwdColMask) * is + 4 * q);
+  };
+  uint32_t c[U], sw[U];
+  float v[U];
+  if constexpr ((U & 3) == 0) {
+    if ((L & 3) == 0) {
+      // lane q of a quad loads the record of sub-step 4j + q (contiguous), DPP hands it on: one
+      // record instruction per four sub-steps. Software-pipelined: per step i the issue order is
+      // selectors of step i+1, records of step i+2, then step i's LDS reads and stores, so no
+      // load's wait covers an older store (vmcnt counts stores with loads in issue order; the
+      // unpipelined loop waited for the previous step's stores before every step's selectors:
+      // ogbn-products k = 32 row pass 5.37 -> 5.25 ms, profiles/r04/tp_rows_pipelined.jsonl).
+      // Every load is clamped to a valid edge of the rows, no branches.
+      const int qq = lane & 3;
+      const int S = EPS * U;
+      auto load_raw = [&](int b, uint2 (&raw)[U / 4]) {
+#pragma unroll
+        for (int j = 0; j < U / 4; ++j)
+          raw[j] = *reinterpret_cast<const uint2*>(
+              erec + 2 * (size_t)min(b + (4 * j + qq) * EPS + slot, e1 - 1));
+      };
+      auto decode = [&](const uint2 (&raw)[U / 4], uint32_t (&cc)[U], float (&vv)[U]) {
+#pragma unroll
+        for (int j = 0; j < U / 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            cc[4 * j + i] = quad_pick(raw[j].x, i);
+            vv[4 * j + i] = __uint_as_float(quad_pick(raw[j].y, i));
+          }
+      };
+      uint2 raw0[U / 4], raw1[U / 4];
+      load_raw(e0, raw0);
+      load_raw(e0 + S, raw1);
+      decode(raw0, c, v);
+      load_sel(c, sw);
+      for (int base = e0; base < e1; base += S) {
+        uint32_t cn[U], swn[U];
+        float vn[U];
+        decode(raw1, cn, vn);
+        load_sel(cn, swn);
+        load_raw(base + 2 * S, raw1);
+        compute_store(base, c, v, sw);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          c[u] = cn[u];
+          v[u] = vn[u];
+          sw[u] = swn[u];
+        }
+      }
+      return;
+    }
+  }
+  for (int base = e0; base < e1; base += EPS * U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = min(base + u * EPS + slot, e1 - 1);
+      const uint2 cv = *reinterpret_cast<const uint2*>(erec + 2 * (size_t)e);
+      c[u] = cv.x;  // column | (row % R) << kFwdColBits
+      v[u] = __uint_as_float(cv.y);
+    }
+    load_sel(c, sw);
+    compute_store(base, c, v, sw);
   }
 }
 
