@@ -407,10 +407,11 @@ static void build_fwd_tasks(const std::vector<int32_t>& hp, int N, int R, int64_
   const int64_t E = hp[N];
   const int ntiles = (N + R - 1) / R;
   const int64_t avg = ntiles ? (E + ntiles - 1) / ntiles : 0;
-  // 2 x the average tile (was 4 x): heavy tiles split into a few more tasks balance the tail
-  // (an 8-GPU row shard of Reddit 0.203 -> 0.195 ms; Reddit k = 8 0.925 -> 0.911, k = 16,
-  // ogbn-products and ogbn-proteins within noise)
-  const int64_t cap = cap_opt > 0 ? cap_opt : std::max<int64_t>(4096, 2 * avg);
+  // 1.5 x the average tile (round 3: 2 x, before that 4 x): heavy tiles split into a few more
+  // tasks balance the tail and keep the tiles running together closer to the rotation clock
+  // (Reddit k = 16 / 32 / 64: 1.096 / 1.689 / 3.131 -> 1.083 / 1.680 / 3.079 ms, k = 8 equal;
+  // 1.25 x is slower, profiles/r04/fwd_task_cap_ab.jsonl)
+  const int64_t cap = cap_opt > 0 ? cap_opt : std::max<int64_t>(4096, avg + avg / 2);
   auto push_rows = [&](int r0, int r1) {
     if (r1 > r0) tasks.push_back(FwdTask{r0, r1 - r0, hp[r0], hp[r1]});
   };
@@ -528,14 +529,14 @@ static int check_options(const maxk_plan_options& o) {
                      o.bwd_unroll == 16,
                  "maxk_plan_create: bwd_unroll must be 0, 8, 12 or 16");
   MAXK_CHECK_REMOVED(o.bwd_order != 1, "bwd_order = 1 (heavy-first tasks)");
-  MAXK_CHECK_ARG(o.bwd_order >= 0 && o.bwd_order <= 2, "maxk_plan_create: bwd_order must be 0 or 2");
+  MAXK_CHECK_ARG(o.bwd_order >= 0 && o.bwd_order <= 3, "maxk_plan_create: bwd_order must be 0, 2 or 3");
   MAXK_CHECK_ARG(o.bwd_slot_groups >= 0 && o.bwd_slot_groups <= 64 &&
                      (o.bwd_slot_groups & (o.bwd_slot_groups - 1)) == 0,
                  "maxk_plan_create: bwd_slot_groups must be 0 or a power of two <= 64");
   MAXK_CHECK_REMOVED(o.bwd_acc_pad == 0 || o.bwd_acc_pad == 2, "bwd_acc_pad = 1");
   MAXK_CHECK_REMOVED(o.bwd_sel_lds == 0 || o.bwd_sel_lds == 1, "bwd_sel_lds = 2");
-  MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 2,
-                 "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 3,
+                 "maxk_plan_create: fwd_rotate must be 0, 1, 2 or 3");
   MAXK_CHECK_ARG(o.bwd_algo >= 0 && o.bwd_algo <= 3,
                  "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks) or 3 (two-pass)");
   MAXK_CHECK_REMOVED(o.bwd_algo != 2, "bwd_algo = 2 (column-major)");
@@ -846,6 +847,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
                                              : std::min(5e8, std::max(2e7, (p->fwd_fixed ? kFwdSlotEdgeRateFixed : kFwdSlotEdgeRate) * 16.0 / k));
       const double tile_ticks = (double)E / nt / rate * 1e8;  // s_memrealtime: 100 MHz
       p->fwd_rot_ticks = (int)std::max(1.0, tile_ticks / B);
+      if (o.fwd_rotate == 3) p->fwd_rot_avg = (int32_t)std::max<int64_t>(1, E / nt);
     }
     B = std::max(1, std::min(B, std::max(NC, 1)));
     p->fwd_phases = B;
@@ -1271,7 +1273,11 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       p->device_bytes += sizeof(int4) * comb.size();
     }
   }
-  if (o.bwd_order == 2 && btasks.size() >= 2 * (size_t)kXcds) {
+  // default on with one slot group (Reddit k = 16: 1.665 -> 1.626 ms, an 8-GPU row shard
+  // 0.241 -> 0.226); with two groups a block's two tasks already share their rows and the
+  // windows measured +0.7-1.5 % (k = 32 / 64, profiles/r04/bwd_order_ab.jsonl)
+  const bool windows = o.bwd_order == 2 || (o.bwd_order == 0 && p->bwd_slot_groups == 1);
+  if (windows && btasks.size() >= 2 * (size_t)kXcds) {
     // XCD row windows: work-group i runs on XCD i % 8, one task per CU at a time. Within each
     // round of `cus` consecutive (row-sorted) tasks, XCD x gets the x-th contiguous run of
     // them, so the work-groups sharing an XCD's L2 sweep one row window of G instead of every

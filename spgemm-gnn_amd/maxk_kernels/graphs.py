@@ -286,6 +286,13 @@ def load_npz_csr(path: str, self_loops: bool = True, device="cpu"):
     return ptr.to(torch.int32), cols.to(torch.int32)
 
 
-def dataset_csr(name: str, device="cpu", seed: int = 97):
+def bench_csr(name: str, device="cpu", seed: int = 97):
+    """(ptr, idx) of the bench graph shaped like dataset ``name``: :func:`synthetic_ptr` +
+    :func:`synthetic_rows` (bench.py's graph at every world size; the tools time this one)."""
     n, e = DATASETS[name]
-    return synthetic_csr(n, e, seed=seed, device=device)
+    ptr = synthetic_ptr(n, e, seed=seed, device=device)
+    return ptr, synthetic_rows(ptr, seed=seed)
+
+
+def dataset_csr(name: str, device="cpu", seed: int = 97):
+    return bench_csr(name, device=device, seed=seed)

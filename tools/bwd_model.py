@@ -67,7 +67,7 @@ def plan_info(root):
 
 def replay(k, C, S, F, samples, seed=5):
     n, e = graphs.DATASETS["reddit"]
-    ptr, idx = graphs.synthetic_csr(n, e)
+    ptr, idx = graphs.bench_csr("reddit")
     e = idx.numel()
     h = graphs.features(n, 256, seed=97)
     sel = torch.sort(torch.topk(h, k, dim=1).indices, dim=1).values.to(torch.int16)

@@ -66,7 +66,7 @@ def main():
 
     # config 2: Reddit forward vs rocSPARSE
     n, e = graphs.DATASETS["reddit"]
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    ptr, idx = graphs.bench_csr("reddit", device=dev)
     val = graphs.sage_mean_values(ptr)
     h = graphs.features(n, d, seed=97, device=dev)
     sp_data, sp_index = mk.maxk_forward(h, 16, return_index=True)
@@ -85,7 +85,7 @@ def main():
 
     # config 3: ogbn-products SAGE, k = 32, autograd path and kernels
     n, e = graphs.DATASETS["ogbn-products"]
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    ptr, idx = graphs.bench_csr("ogbn-products", device=dev)
     val = graphs.sage_mean_values(ptr)
     h = graphs.features(n, d, seed=97, device=dev)
     g = graphs.features(n, d, seed=98, device=dev)
@@ -106,7 +106,7 @@ def main():
 
     # config 4: ogbn-proteins GCN, k sweep
     n, e = graphs.DATASETS["ogbn-proteins"]
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    ptr, idx = graphs.bench_csr("ogbn-proteins", device=dev)
     val = graphs.gcn_values(ptr, idx)
     h = graphs.features(n, d, seed=97, device=dev)
     g = graphs.features(n, d, seed=98, device=dev)

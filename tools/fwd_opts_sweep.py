@@ -1,5 +1,5 @@
 """Forward plan-option sweep on the Reddit-shaped graph (tooling): HIP-event ms per
-option set, with the plan's task count.
+option set (interleaved rounds, median), with the plan's task count.
   python tools/fwd_opts_sweep.py --k 16 --opts '[{}, {"fwd_rot_rate": 200}]'"""
 import argparse
 import json
@@ -31,27 +31,29 @@ def main():
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--dataset", default="reddit")
     ap.add_argument("--opts", default='[{}]')
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS[args.dataset]
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    ptr, idx = graphs.bench_csr(args.dataset, device=dev)
     val = graphs.sage_mean_values(ptr)
     e = idx.numel()
     h = graphs.features(n, 256, seed=97, device=dev)
     sd, si = mk.maxk_forward(h, args.k, return_index=True)
-    ref = None
-    for opts in json.loads(args.opts):
-        plan = mk.GraphPlan(ptr, idx, val, n, e, 256, args.k, options=opts)
-        gr = torch.empty((n, 256), device=dev)
-        t = timeit(lambda: plan.forward(sd, si, gr))
-        if ref is None:
-            ref = gr.clone()
-        info = plan.info()
-        print(json.dumps({"k": args.k, "opts": opts, "fwd_ms": round(t, 4), "tasks": info["fwd_tasks"],
-                          "max_rel_dev": float(((gr - ref).abs() / (ref.abs() + 1e-3)).max())}),
+    sets = json.loads(args.opts)
+    plans = [mk.GraphPlan(ptr, idx, val, n, e, 256, args.k, options=o) for o in sets]
+    outs = [torch.empty((n, 256), device=dev) for _ in sets]
+    times = [[] for _ in sets]
+    for _ in range(args.rounds):  # interleaved, so box drift hits every set alike
+        for i, plan in enumerate(plans):
+            times[i].append(timeit(lambda: plan.forward(sd, si, outs[i])))
+    for i, opts in enumerate(sets):
+        t = sorted(times[i])
+        dev_max = float(((outs[i] - outs[0]).abs() / (outs[0].abs() + 1e-3)).max())
+        print(json.dumps({"k": args.k, "opts": opts, "fwd_ms": round(t[len(t) // 2], 4),
+                          "fwd_ms_all": [round(x, 4) for x in times[i]],
+                          "tasks": plans[i].info()["fwd_tasks"], "max_rel_dev": dev_max}),
               flush=True)
-        del plan
-
 
 if __name__ == "__main__":
     main()

@@ -48,7 +48,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS["reddit"]
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    ptr, idx = graphs.bench_csr("reddit", device=dev)
     val = graphs.sage_mean_values(ptr)
     d, k = 256, args.k
     h = graphs.features(n, d, seed=97, device=dev)

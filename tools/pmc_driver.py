@@ -20,7 +20,7 @@ dev = torch.device("cuda:0")
 n, e = graphs.DATASETS[ds]
 shape = os.environ.get("PMC_GRAPH", "uniform")
 if shape == "uniform":
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    ptr, idx = graphs.bench_csr(ds, device=dev)
 else:
     ptr, idx = graphs.community_csr(n, e, shuffle=shape == "shuffled", device=dev)
 val = graphs.sage_mean_values(ptr) if kind == "sage" else graphs.gcn_values(ptr, idx)

@@ -23,7 +23,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS[args.dataset]
-    ptr, idx = graphs.synthetic_csr(n, e, device=dev)
+    ptr, idx = graphs.bench_csr(args.dataset, device=dev)
     val = graphs.sage_mean_values(ptr)
     h = graphs.features(n, 256, seed=97, device=dev)
     g = graphs.features(n, 256, seed=98, device=dev)
