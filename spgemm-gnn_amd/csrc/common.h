@@ -167,7 +167,6 @@ struct maxk_plan {
   maxk::FwdTask* fwd_tasks = nullptr;   // e0/e1 index the permuted edge order below
   int32_t fwd_phases = 1;        // column windows of the rotated sweep (1: no rotation)
   int32_t fwd_rot_ticks = 0;     // > 0: rotated sweeps, s_memrealtime ticks per window
-  int32_t fwd_rot_avg = 0;       // > 0: per-size clocks (fwd_rotate 3), average task edges
   int32_t fwd_chunk3 = 0;        // lane-chunk records: 3 values + their selectors per 16 B
   int32_t fwd_quad = 0;          // quad-shared edge-word loads
   int32_t fwd_two_tables = 0;    // gather from sp_data / sp_index directly (no pack)

@@ -535,8 +535,8 @@ static int check_options(const maxk_plan_options& o) {
                  "maxk_plan_create: bwd_slot_groups must be 0 or a power of two <= 64");
   MAXK_CHECK_REMOVED(o.bwd_acc_pad == 0 || o.bwd_acc_pad == 2, "bwd_acc_pad = 1");
   MAXK_CHECK_REMOVED(o.bwd_sel_lds == 0 || o.bwd_sel_lds == 1, "bwd_sel_lds = 2");
-  MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 3,
-                 "maxk_plan_create: fwd_rotate must be 0, 1, 2 or 3");
+  MAXK_CHECK_ARG(o.fwd_rotate >= 0 && o.fwd_rotate <= 2,
+                 "maxk_plan_create: fwd_rotate must be 0, 1 or 2");
   MAXK_CHECK_ARG(o.bwd_algo >= 0 && o.bwd_algo <= 3,
                  "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks) or 3 (two-pass)");
   MAXK_CHECK_REMOVED(o.bwd_algo != 2, "bwd_algo = 2 (column-major)");
@@ -847,7 +847,6 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
                                              : std::min(5e8, std::max(2e7, (p->fwd_fixed ? kFwdSlotEdgeRateFixed : kFwdSlotEdgeRate) * 16.0 / k));
       const double tile_ticks = (double)E / nt / rate * 1e8;  // s_memrealtime: 100 MHz
       p->fwd_rot_ticks = (int)std::max(1.0, tile_ticks / B);
-      if (o.fwd_rotate == 3) p->fwd_rot_avg = (int32_t)std::max<int64_t>(1, E / nt);
     }
     B = std::max(1, std::min(B, std::max(NC, 1)));
     p->fwd_phases = B;

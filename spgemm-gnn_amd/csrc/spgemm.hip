@@ -421,8 +421,7 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     const FwdTask* __restrict__ tasks, const int32_t* __restrict__ phase_off, int phases,
     const uint2* __restrict__ cv, const float* __restrict__ sp_data,
     const uint8_t* __restrict__ sp_index, const uint8_t* __restrict__ rec, int rec_bytes,
-    float* __restrict__ out, int D, int k, int rot_ticks, int rot_avg,
-    const uint8_t* __restrict__ seltab,
+    float* __restrict__ out, int D, int k, int rot_ticks, const uint8_t* __restrict__ seltab,
     int ss, int ds, int accum, const int2* __restrict__ fix_tab,
     const uint32_t* __restrict__ xstat, int xs_n, int xs_stride, int xs_off2) {
   extern __shared__ __align__(16) double smem_d[];
@@ -436,19 +435,8 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   int emid = -1;
   if (rot_ticks > 0) {
     // read once per work-group: every wave must split the task at the same edge
-    if (threadIdx.x == 0) {
-      uint64_t ticks = (uint64_t)rot_ticks;
-      if (rot_avg > 0) {
-        // per-size clocks: a task r times the average sweeps a window in r x the average
-        // time, so it follows a clock r x slower; sizes are rounded to classes of 2^(1/8),
-        // whose tasks share one clock and stay in phase (heavy-first order keeps the tasks
-        // running together in one or two classes)
-        const float r = fmaxf((float)(t.e1 - t.e0) / (float)rot_avg, 1.f / 64.f);
-        const float q = exp2f(rintf(8.f * log2f(r)) * 0.125f);
-        ticks = (uint64_t)fmaxf(1.f, (float)rot_ticks * q);
-      }
-      s_w0 = (int)((__builtin_amdgcn_s_memrealtime() / ticks) % (uint64_t)phases);
-    }
+    if (threadIdx.x == 0)
+      s_w0 = (int)((__builtin_amdgcn_s_memrealtime() / (uint64_t)rot_ticks) % (uint64_t)phases);
     __syncthreads();
     emid = phase_off[ti * (phases + 1) + s_w0];
   }
@@ -1253,8 +1241,7 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     hipLaunchKernelGGL((spgemm_fwd_kernel<V, FF>), dim3(plan->n_fwd_tasks), dim3(kFwdThreads), \
                        lds, s, plan->fwd_tasks, plan->fwd_phase_off, plan->fwd_phases,      \
                        plan->fwd_cv, sp_data, sp_index, recp, rec_bytes, out, D, k,         \
-                       plan->fwd_rot_ticks, plan->fwd_rot_avg, seltab, is, ds, accum,      \
-                       fix_tab, xstat, xs_n,                                                \
+                       plan->fwd_rot_ticks, seltab, is, ds, accum, fix_tab, xstat, xs_n,     \
                        xs_stride, xs_off2);                                                 \
   } while (0)
   if (k % 4 == 0 || plan->fwd_chunk3) {
