@@ -32,7 +32,9 @@ constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k stores) vs its
 constexpr int kXcds = 8;
 constexpr int kFwdRotWindows = 16;         // column windows of the rotated forward sweep
 constexpr double kFwdSlotEdgeRate = 1.6e8;  // edges/s one forward slot sustains at k = 16
-constexpr double kFwdSlotEdgeRateFixed = 2.6e8;  // the same with the fixed-point update
+constexpr double kFwdSlotEdgeRateFixed = 3.0e8;  // the same with the fixed-point update
+// (round 4: 2.6e8 -> 3.0e8 with the 1.5 x task cap, Reddit k = 16 / 32 / 64 -1.0 / -0.2 / -0.3 %;
+// 3.5e8 and above slower, profiles/r04/fwd_rot_rate_ab.jsonl)
 // CBSR tables (5k bytes per column) above these sizes get packed one-line forward records
 // even where two tables would otherwise be used (plan.hip: k >= 32 / k < 32)
 constexpr double kFwdPackedTableBytes = 150e6;
