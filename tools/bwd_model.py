@@ -18,11 +18,11 @@ HBM), split with the measured TCP_TCC_READ_REQ per gather instruction and TCC hi
   python tools/bwd_model.py --k 16 --block-cols 1821 --groups 1 --pmc gpurun_out/pmc_model_reddit_k16
 """
 import argparse
+import ast
 import csv
 import glob
 import json
 import os
-import re
 import sys
 from collections import defaultdict
 
@@ -61,7 +61,7 @@ def plan_info(root):
     for f in sorted(glob.glob(os.path.join(root, "pass*.log"))):
         for line in open(f):
             if line.startswith("done "):
-                return eval(line[5:], {"__builtins__": {}})  # noqa: S307 (our own dict repr)
+                return ast.literal_eval(line[5:])
     return None
 
 

@@ -7,7 +7,7 @@ Reddit-sized graphs with and without column locality, for a list of plan option 
 
 Prints one JSON line per (graph, k, option set): E, plan build s, fwd/bwd ms (HIP events,
 median of 5 x 10), the algorithmic-byte roofline fraction of each kernel, and the plan info.
-  python tools/locality_graphs.py [--k 16,32] [--opts '[{}, {"col_order": 3}]']"""
+  python tools/locality_graphs.py [--k 16,32] [--opts '[{}, {"col_order": 2}]']"""
 import argparse
 import json
 import os

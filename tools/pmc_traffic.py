@@ -105,7 +105,7 @@ def main():
     ap.add_argument("--all", action="store_true",
                     help="root holds pmc_<dataset>_<kind>_k<k> directories")
     ap.add_argument("--locality", action="store_true",
-                    help="root holds pmc_loc_<graph>_<order>_k<k> directories (tools/pmc_locality.sh)")
+                    help="root holds pmc_loc_<graph>_<order>_k<k> directories (round 3; pmc_loc_* passes over tools/pmc_driver.py)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
