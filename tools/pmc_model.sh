@@ -1,7 +1,7 @@
 #!/bin/bash
 # Counters behind the backward bound model and the two-pass byte budget
-# (tooling): for each dataset:kind:k of PMC_CONFIGS, three rocprofv3 --pmc passes over
-# tools/pmc_driver.py (instruction mix + LDS; texture path + L1 misses; L2 and fabric / DRAM
+# (tooling): for each dataset:kind:k of PMC_CONFIGS, four rocprofv3 --pmc passes over
+# tools/pmc_driver.py (instruction mix + LDS; texture path + L1 misses; L2 hits and fabric
 # requests; writes), each its own run with --kernel-trace only. Output gpurun_out/pmc_model_<tag>/;
 # summarise with  python tools/pmc_group.py gpurun_out/pmc_model_<tag>
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
