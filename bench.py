@@ -24,13 +24,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spgemm-gnn_amd"))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
+# numpy, torch and maxk_kernels are imported by _imports() once the process knows it is a
+# rank: a bare `bench.py --gpus N` (N > 1) parent spawns the ranks and never touches HIP
+np = torch = dist = mk = graphs = RowPartition = ShardedAggregation = None
 
-import maxk_kernels as mk  # noqa: E402
-from maxk_kernels import graphs  # noqa: E402
-from maxk_kernels.dist import RowPartition, ShardedAggregation  # noqa: E402
+
+def _imports():
+    global np, torch, dist, mk, graphs, RowPartition, ShardedAggregation
+    import numpy as _np
+    import torch as _torch
+    import torch.distributed as _dist
+
+    import maxk_kernels as _mk
+    from maxk_kernels import graphs as _graphs
+    from maxk_kernels.dist import RowPartition as _RP, ShardedAggregation as _SA
+    np, torch, dist, mk, graphs = _np, _torch, _dist, _mk, _graphs
+    RowPartition, ShardedAggregation = _RP, _SA
+
 
 # BASELINE.json "metric", verbatim: the primary line is k=16 (config.workload), the other k
 # of the set are the k_sweep entries
@@ -94,10 +104,13 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d, sample_frac, reps, log_fn):
+def cpu_baseline(ptr, idx, val, sp_data, sp_index, h, g, d, sample_frac, runs, warmup, log_fn):
     """DGL-semantics dense CSR SpMM on the host cores (oracle C/OpenMP restatement of
-    update_all(copy_u, sum) with edge weights; the dense MaxK output as DGL sees it),
-    forward A @ X and backward A^T @ G, on a bounded sample of the destination rows."""
+    update_all(copy_u, sum) with edge weights), forward A @ X and backward A^T @ G, on a
+    bounded sample of the destination rows, by BASELINE.md §3's protocol: `warmup` untimed
+    runs, then the median of `runs` timed runs. Two inputs, as §3 lists them: (a) the dense
+    MaxK output, zeros included, as DGL sees it (`value`), and (b) the ReLU of the layer
+    input, the reference's ReLU baseline (`relu_value`)."""
     from oracle import oracle
 
     n = ptr.numel() - 1
@@ -112,61 +125,87 @@ def cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d, sample_frac, reps, log_
     cnt = torch.bincount(idx.long(), minlength=n)
     ptr_t = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     ptr_t[1:] = torch.cumsum(cnt, 0)
-    h = {k: v.cpu().numpy() for k, v in dict(ptr=ptr, idx=idx, val=val, x=x, g=g,
+    hh = {k: v.cpu().numpy() for k, v in dict(ptr=ptr, idx=idx, val=val, x=x,
+                                                relu=torch.relu(h), g=g,
                                                 ptr_t=ptr_t.to(torch.int32), idx_t=idx_t,
                                                 val_t=val_t).items()}
     del x, order, rows, idx_t, val_t, cnt, ptr_t
-    e = int(h["ptr"][-1])
+    e = int(hh["ptr"][-1])
     target = int(e * sample_frac)
-    r_f = int(np.searchsorted(h["ptr"], target))
-    r_b = int(np.searchsorted(h["ptr_t"], target))
+    r_f = int(np.searchsorted(hh["ptr"], target))
+    r_b = int(np.searchsorted(hh["ptr_t"], target))
+    e_f, e_b = int(hh["ptr"][r_f]), int(hh["ptr_t"][r_b])
     y = np.zeros((n, d), np.float32)
-    # warm-up on a small slice (page-in), then the timed sample
-    oracle.dense_spmm(h["ptr"], h["idx"], h["val"], h["x"], row_end=min(n, 2000), out=y)
-    tf = tb = 0.0
-    for _ in range(reps):
+
+    def one(feat):
         t0 = time.perf_counter()
-        oracle.dense_spmm(h["ptr"], h["idx"], h["val"], h["x"], row_end=r_f, out=y)
+        oracle.dense_spmm(hh["ptr"], hh["idx"], hh["val"], hh[feat], row_end=r_f, out=y)
         t1 = time.perf_counter()
-        oracle.dense_spmm(h["ptr_t"], h["idx_t"], h["val_t"], h["g"], row_end=r_b, out=y)
-        t2 = time.perf_counter()
-        tf += t1 - t0
-        tb += t2 - t1
-    e_f, e_b = int(h["ptr"][r_f]), int(h["ptr_t"][r_b])
-    log_fn(f"cpu baseline: {reps}x fwd {e_f} edges in {tf:.2f}s, bwd {e_b} edges in {tb:.2f}s")
+        oracle.dense_spmm(hh["ptr_t"], hh["idx_t"], hh["val_t"], hh["g"], row_end=r_b, out=y)
+        return t1 - t0, time.perf_counter() - t1
+
+    res = {}
+    for feat in ("x", "relu"):
+        for _ in range(warmup):
+            one(feat)
+        t = [one(feat) for _ in range(runs)]
+        tot = sorted(a + b for a, b in t)
+        med = float(np.median(tot))
+        res[feat] = {"median_s": med, "fwd_s": float(np.median([a for a, _ in t])),
+                     "bwd_s": float(np.median([b for _, b in t])),
+                     "min_s": tot[0], "max_s": tot[-1], "value": (e_f + e_b) / med}
+        log_fn(f"cpu baseline ({feat}): median of {runs} after {warmup} warm-ups: "
+               f"{med:.3f}s for fwd {e_f} + bwd {e_b} edges")
+    affinity = len(os.sched_getaffinity(0))
+    threads = oracle.num_threads()
     return {
-        "value": reps * (e_f + e_b) / (tf + tb),
+        "value": res["x"]["value"],
         "unit": "edges/s",
-        "cores": oracle.num_threads(),
+        "cores": threads,
+        "threads": threads,
+        "relu_value": res["relu"]["value"],
+        "median_of": runs,
+        "warmup_runs": warmup,
         "cpu_model": cpu_model(),
         "host_cpus": os.cpu_count(),
-        "affinity_cpus": len(os.sched_getaffinity(0)),
-        "cores_note": ("OpenMP threads = the lease's CPU share (OMP_NUM_THREADS, set by the GPU "
-                       "pool per GPU; host_cpus / affinity_cpus count the whole machine)"),
+        "affinity_cpus": affinity,
+        "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+        "threads_reason": (
+            "OpenMP threads = OMP_NUM_THREADS, the CPU share the GPU pool leases with one "
+            "GPU (16 on the MI355X boxes). The affinity mask spans the whole machine "
+            f"({affinity} CPUs), shared with the other leases' jobs, so more threads would "
+            "time other tenants' load, not this path"
+            if os.environ.get("OMP_NUM_THREADS") else
+            "OpenMP default: every CPU in the affinity mask"),
         "kind": "port",
         "sample": (f"DGL-semantics dense CSR SpMM (oracle C/OpenMP, f32): forward A@X over "
                    f"rows [0,{r_f}) = {e_f} edges and backward A^T@G over rows [0,{r_b}) of "
                    f"the transposed graph = {e_b} edges ({sample_frac:.0%} of E each), "
-                   f"D={d}, X = dense MaxK output, {reps} repetitions"),
-        "fwd_s": tf / reps,
-        "bwd_s": tb / reps,
+                   f"D={d}; value: X = dense MaxK output, relu_value: X = ReLU(layer input); "
+                   f"median of {runs} runs after {warmup} warm-ups (BASELINE.md §3)"),
+        "fwd_s": res["x"]["fwd_s"],
+        "bwd_s": res["x"]["bwd_s"],
+        "runs": res,
     }
 
 
-def main():
-    if os.environ.get("MAXK_BENCH_TRACEBACK_S"):  # where a stuck rank is (rehearsals)
-        import faulthandler
-        faulthandler.dump_traceback_later(float(os.environ["MAXK_BENCH_TRACEBACK_S"]), repeat=True)
+# graphs.DATASETS keys, here so the arguments parse before torch is imported (checked in run)
+DATASET_NAMES = ("flickr", "ogbn-products", "ogbn-proteins", "reddit", "yelp")
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--dataset", default="reddit", choices=sorted(graphs.DATASETS))
+    ap.add_argument("--dataset", default="reddit", choices=DATASET_NAMES)
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--dim", type=int, default=256)
-    ap.add_argument("--cpu-sample", type=float, default=1.0,
-                    help="fraction of E timed per direction for the CPU baseline")
-    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=float, default=0.1,
+                    help="fraction of E timed per direction and run for the CPU baseline")
+    ap.add_argument("--cpu-runs", type=int, default=10,
+                    help="timed CPU runs (the median is reported; BASELINE.md §3)")
+    ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-comparator", action="store_true")
     ap.add_argument("--k-sweep", default="8,32,64",
@@ -175,8 +214,123 @@ def main():
                     help="'synthetic', 'auto' (the DGL cache file ~/.dgl/... when it exists, "
                          "else synthetic) or a path to a scipy save_npz adjacency")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, poll_s=0.2, grace_s=10.0):
+    """`bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment): start N
+    rank processes of this script with the torch.distributed.run environment (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), relay rank 0's stdout
+    (the JSON line), and return 0 when every rank exits 0. When a rank fails, the others
+    (which may be waiting in a collective for it) are terminated by PID and the failing
+    rank's exit code is returned. This process imports neither torch nor maxk_kernels, so it
+    never initialises HIP before the children start (an exec or fork after HIP init is not
+    safe on this platform)."""
+    import signal
+    import subprocess
+    import threading
+
+    assert "torch" not in sys.modules, "the spawning parent must not import torch"
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    base = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                ROLE_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                MAXK_BENCH_SPAWNED="1")
+    print(f"[bench] spawning {n} ranks on 127.0.0.1:{port} (parent imports no torch)",
+          file=sys.stderr, flush=True)
+    procs = []
+
+    def stop(sig=None, frame=None):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        if sig is not None:
+            sys.exit(128 + sig)
+
+    old_term = signal.signal(signal.SIGTERM, stop)
+    relay = None
+    try:
+        for r in range(n):
+            env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                          env=env,
+                                          stdout=subprocess.PIPE if r == 0 else None,
+                                          text=True))
+
+        def pump(f):
+            for line in f:
+                sys.stdout.write(line)
+                sys.stdout.flush()
+
+        relay = threading.Thread(target=pump, args=(procs[0].stdout,), daemon=True)
+        relay.start()
+        rc = 0
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                i, rc = bad[0]
+                print(f"[bench] rank {i} exited with {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop()
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        stop()
+        if relay is not None:
+            relay.join(timeout=5)
+        signal.signal(signal.SIGTERM, old_term)
+    return rc if rc >= 0 else 128 - rc
+
+
+def _selftest_rank(spec):
+    """MAXK_BENCH_SELFTEST (tests/test_bench_spawn.py): a rank that only reports what the
+    launcher handed it, without torch. 'ok': rank 0 prints one JSON line. 'fail:R': rank R
+    exits 3 and the others hang (as ranks stuck in a collective would)."""
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if spec.startswith("fail:"):
+        if rank == int(spec.split(":", 1)[1]):
+            time.sleep(0.5)
+            sys.exit(3)
+        time.sleep(600)
+    if rank == 0:
+        print(json.dumps({"selftest": True, "world": world, "rank": rank,
+                          "local_rank": int(os.environ["LOCAL_RANK"]),
+                          "master": f"{os.environ['MASTER_ADDR']}:{os.environ['MASTER_PORT']}",
+                          "spawned": os.environ.get("MAXK_BENCH_SPAWNED") == "1"}), flush=True)
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if os.environ.get("MAXK_BENCH_SELFTEST"):
+        _selftest_rank(os.environ["MAXK_BENCH_SELFTEST"])
+        return
+    _imports()
+    assert set(DATASET_NAMES) == set(graphs.DATASETS), "DATASET_NAMES out of date"
+    run(args)
+
+
+def run(args):
+    if os.environ.get("MAXK_BENCH_TRACEBACK_S"):  # where a stuck rank is (rehearsals)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["MAXK_BENCH_TRACEBACK_S"]), repeat=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -524,8 +678,9 @@ def main():
         del x
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(ptr, idx, val, sp_data, sp_index, g, d,
-                                              args.cpu_sample, args.cpu_reps, log)
+        result["cpu_baseline"] = cpu_baseline(ptr, idx, val, sp_data, sp_index, h, g, d,
+                                              args.cpu_sample, args.cpu_runs, args.cpu_warmup,
+                                              log)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -196,7 +196,7 @@ struct maxk_plan {
   int32_t n_bwd_shared = 0;
   int32_t* bwd_perm = nullptr;   // CSR edge id of each reordered edge
   uint32_t* bwd_rec = nullptr;   // [num_edges + kBwdRecPad][3]
-  uint32_t* bwd_sel = nullptr;   // plan-owned workspace: [S][num_cols][L] selector words + slabs
+  uint32_t* bwd_sel = nullptr;   // plan-owned workspace: the slabs (bwd_slab_floats)
   // two-pass backward (low row reuse): a row pass writes each edge's k products val *
   // grad_out[r, sel(c)] into the edge's slot of bwd_tbuf (CSR order), a column pass sums the
   // slots of each column's in-edges (bwd_perm, bwd_colptr)

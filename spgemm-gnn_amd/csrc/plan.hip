@@ -467,8 +467,9 @@ extern "C" int maxk_plan_create_ex(const int32_t* ptr, const int32_t* idx, const
                                    int32_t N, int32_t NC, int64_t E, int32_t D, int32_t k,
                                    const maxk_plan_options* opts, void* stream,
                                    maxk_plan** out_plan) {
-  // the last layout shipped under ABI 1 (through bwd_tp_store, 144 bytes); a binding of the
-  // round-1 120-byte layout passes its size to maxk_plan_create_sized
+  // the round-1 layout create_ex shipped with (through fwd_rot_rate, 120 bytes): reading the
+  // later 144-byte ABI-1 layout here would read 24 bytes past a round-1 caller's struct.
+  // Fields from offset 120 on are set through maxk_plan_create_sized
   return maxk_plan_create_sized(ptr, idx, val, N, NC, E, D, k, opts,
                                 opts ? MAXK_PLAN_OPTIONS_V1_BYTES : 0, nullptr, stream, out_plan);
 }
@@ -1306,11 +1307,12 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->bwd_perm,
                        brow, bcol, val, E, C, D, p->bwd_big, p->bwd_rec);
     PLAN_TRY(hipGetLastError());
-    // per-call workspace: lane-ordered selector words (kp bytes per column), then the slabs
-    const int64_t sel_bytes = (int64_t)std::max(NC, 1) * p->bwd_kp;
-    p->bwd_slab_off = (sel_bytes + 255) / 256 * 256;
-    p->bwd_ws_bytes = p->bwd_slab_floats > 0 ? p->bwd_slab_off + p->bwd_slab_floats * 4 : sel_bytes;
-    if (!p->external_ws) PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)p->bwd_ws_bytes));
+    // per-call workspace: the slab regions of split blocks (the kernel stages the selectors
+    // from sp_index itself; no selector words since round 5)
+    p->bwd_slab_off = 0;
+    p->bwd_ws_bytes = p->bwd_slab_floats * 4;
+    if (!p->external_ws && p->bwd_ws_bytes > 0)
+      PLAN_TRY(hipMalloc(&p->bwd_sel, (size_t)p->bwd_ws_bytes));
     p->device_bytes += (int64_t)E * 16 + 12ll * kBwdRecPad + (!p->external_ws ? p->bwd_ws_bytes : 0);
   }
   PLAN_TRY(hipStreamSynchronize(s));

@@ -541,39 +541,19 @@ __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, fl
 // --------------------------------------------------------------------------------------
 // backward: column blocks
 // --------------------------------------------------------------------------------------
-// Selector words in lane order (per call): word (g * n + c) * L + q of the F-slot kernel holds
-// the F selectors of lane q of column position c in slot group g, slots g * ns + q + L * i
-// (i = 0 .. F-1, L = ns / F lanes, ns = kp / S slots per group), as F bytes. Slots >= k (the
-// padding up to kp) select feature 0; their accumulators are never stored.
-template <int F>
-__global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int is, int n, int k,
-                                int kp, int S,
-                                std::conditional_t<F == 4, uint32_t, uint16_t>* __restrict__ sel,
-                                const int32_t* __restrict__ corder) {
-  const int ns = kp / S;
-  const int L = ns / F;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n * L * S) return;
-  const int g = i / (n * L);
-  const int r = i - g * (n * L);
-  const int c = r / L, q = r - c * L;
-  const uint8_t* s = sp_index + (size_t)(corder ? corder[c] : c) * is;
-  uint32_t w = 0u;
-#pragma unroll
-  for (int j = 0; j < F; ++j) {
-    const int l = g * ns + q + L * j;
-    w |= (uint32_t)(l < k ? s[l] : 0u) << (8 * j);
-  }
-  sel[i] = (std::conditional_t<F == 4, uint32_t, uint16_t>)w;
-}
-
 // One work-group per (column block, row chunk piece, slot group) task, NT threads (8 waves,
 // 12 at k >= 32: more gathers in flight per CU under the same LDS block). Lanes: L = ns / F
 // per edge, lane q owns the F slots q, q + L, ... of its group, stored adjacently in LDS
 // (slot l of a column at (l % L) * F + l / L), so an update is 1 ds_read_b128 + 2
 // ds_cmpst_rtn_b64 (F = 4) or 1 ds_read_b64 + 1 ds_cmpst_rtn_b64 (F = 2); a pair is retried
-// if either of its floats changed. The block's selector words are staged in LDS behind the
-// accumulators (the G rows evict the block's 16 B/column table from the 32 KB L1).
+// if either of its floats changed. The block's selectors are staged in LDS behind the
+// accumulators (the G rows evict the block's 16 B/column table from the 32 KB L1), straight
+// from sp_index rows (row stride `is` bytes, column corder[position] when the plan has a
+// column order): dword loads of 4 selectors, scattered into lane order, so slot l of the
+// group (global slot g * ns + l; >= k is padding and selects feature 0) lands in byte
+// (c * L + l % L) * F + l / L and lane q reads its F selectors as one word. (Rounds 1-4 packed
+// the lane-ordered words in a per-call pass, pack_sel_kernel: 7-9 us and one launch per call;
+// round 3's in-kernel staging with byte gathers had cost more than that pass.)
 // Per sub-step a lane loads its edge's record {row offset, column in block, val} (Q: lane q
 // of a quad loads sub-step 4j + q's whole record, DPP hands it on: one record instruction
 // per four sub-steps), reads its selector word from LDS and gathers F floats of the edge's
@@ -583,9 +563,8 @@ __global__ void pack_sel_kernel(const uint8_t* __restrict__ sp_index, int is, in
 template <int U, int NT, int F, bool Q, bool BIG>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
-    const float* __restrict__ G, uint32_t g_bytes, int D,
-    const std::conditional_t<F == 4, uint32_t, uint16_t>* __restrict__ sel,
-    float* __restrict__ grad_sp, int k, int ns, int ncols_all, float* __restrict__ slab,
+    const float* __restrict__ G, uint32_t g_bytes, int D, const uint8_t* __restrict__ sp_index,
+    int is, float* __restrict__ grad_sp, int k, int ns, float* __restrict__ slab,
     const int32_t* __restrict__ corder) {
   static_assert(F == 2 || F == 4, "2 or 4 slots per lane");
   static_assert(!Q || U % 4 == 0, "quad record loads need U % 4 == 0");
@@ -600,9 +579,31 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const int KS = ns;      // accumulator floats per column
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
-  const SelT* selg = sel + ((size_t)t.group * ncols_all + t.col0) * L;
   SelT* sell = reinterpret_cast<SelT*>(bacc + ((nacc + 3) & ~3));
-  for (int i = threadIdx.x; i < t.ncols * L; i += NT) sell[i] = selg[i];
+  {
+    uint8_t* sb = reinterpret_cast<uint8_t*>(sell);
+    const int g0 = t.group * ns;
+    auto put = [&](int c, int l, uint32_t v) { sb[(c * L + l % L) * F + l / L] = (uint8_t)v; };
+    if (((is | k | ns | (int)(reinterpret_cast<uintptr_t>(sp_index) & 3)) & 3) == 0) {
+      // 4 selectors per load: a dword never straddles k (k % 4 == 0), so it is all slots or
+      // all padding
+      const int W4 = ns >> 2;
+      for (int i = threadIdx.x; i < t.ncols * W4; i += NT) {
+        const int c = i / W4, l0 = 4 * (i - c * W4);
+        const int col = corder ? corder[t.col0 + c] : t.col0 + c;
+        const uint32_t w = g0 + l0 < k
+            ? *reinterpret_cast<const uint32_t*>(sp_index + (size_t)col * is + g0 + l0) : 0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) put(c, l0 + b, (w >> (8 * b)) & 0xffu);
+      }
+    } else {
+      for (int i = threadIdx.x; i < t.ncols * ns; i += NT) {
+        const int c = i / ns, l = i - c * ns;
+        const int col = corder ? corder[t.col0 + c] : t.col0 + c;
+        put(c, l, g0 + l < k ? sp_index[(size_t)col * is + g0 + l] : 0u);
+      }
+    }
+  }
   __syncthreads();
 
   const int EPS = kWave / L;
@@ -1410,17 +1411,8 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   if (plan->n_bwd_tasks == 0 || (plan->n_bwd_shared > 0 && !slab))
     MAXK_HIP_TRY(hipMemsetAsync(grad_sp, 0, (size_t)NC * k * sizeof(float), s));
   if (plan->n_bwd_tasks == 0) return MAXK_OK;
-  const int F = plan->bwd_feats, S = plan->bwd_slot_groups, ns = plan->bwd_ks;
+  const int F = plan->bwd_feats, ns = plan->bwd_ks;
   const int L = ns / F;
-  const int nsel = NC * L * S;
-  if (F == 4)
-    hipLaunchKernelGGL(pack_sel_kernel<4>, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index, is,
-                       NC, k, plan->bwd_kp, S, sel_ws, plan->bwd_corder);
-  else
-    hipLaunchKernelGGL(pack_sel_kernel<2>, dim3((nsel + 255) / 256), dim3(256), 0, s, sp_index, is,
-                       NC, k, plan->bwd_kp, S, reinterpret_cast<uint16_t*>(sel_ws),
-                       plan->bwd_corder);
-  MAXK_LAUNCH_CHECK("pack_sel launch");
   const uint32_t g_bytes = plan->bwd_big ? 0u : (uint32_t)((uint64_t)N * D * 4u);
   const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, ns);
   const dim3 grid(plan->n_bwd_tasks);
@@ -1428,12 +1420,10 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   const int U = plan->bwd_unroll, W = plan->bwd_waves;
 #define BWD_LAUNCH(UU, NT, FF, QQ, BB)                                                      \
   do {                                                                                      \
-    using SelT = std::conditional_t<FF == 4, uint32_t, uint16_t>;                          \
     if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, FF, QQ, BB>, lds)); \
     hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, FF, QQ, BB>), grid, dim3(NT), lds, s,     \
-                       plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, D,                \
-                       reinterpret_cast<const SelT*>(sel_ws), grad_sp, k, ns, NC, slab,     \
-                       plan->bwd_corder);                                                   \
+                       plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, D, sp_index, is,  \
+                       grad_sp, k, ns, slab, plan->bwd_corder);                             \
   } while (0)
 #define BWD_SHAPES(FF, QQ)                                                                  \
   do {                                                                                      \

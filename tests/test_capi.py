@@ -229,8 +229,8 @@ def test_plan_create_sized_option_sizes():
     assert lib.maxk_plan_create_sized(*args, ctypes.cast(bigger, ctypes.c_void_p), size + 8,
                                       None, None, ctypes.byref(h)) == -1
     assert "null pointer" in lib.maxk_last_error().decode()   # ... then ptr = NULL is refused
-    # the version-1 layout is 144 bytes (up to bwd_tp_store; the round-1 layout ended at
-    # fwd_rot_rate, 120 bytes)
+    # create_ex reads the round-1 layout: 120 bytes, up to fwd_rot_rate; external_workspace ..
+    # bwd_tp_store (offsets 120..143) and the ABI-2 fields only through create_sized
     assert _lib.PlanOptions.bwd_flush.offset == 31 * 4 and _lib.PlanOptions.external_workspace.offset == 120
     assert _lib.PlanOptions.bwd_row_cost.offset == 144
     # an ABI-2 option (col_order = 4) needs the permutation argument
@@ -257,7 +257,7 @@ def test_header_enums_match_binding():
     ba = _header_enum("MAXK_BWD_")
     assert {k.replace("MAXK_BWD_", "").lower(): v for k, v in ba.items()} == _lib.BWD_ALGOS
     v1 = int(re.search(r"#define MAXK_PLAN_OPTIONS_V1_BYTES (\d+)", open(HEADER).read()).group(1))
-    assert v1 == _lib.PlanOptions.bwd_row_cost.offset == 144
+    assert v1 == _lib.PlanOptions.external_workspace.offset == 120
 
 
 def test_removed_options_refused_on_host():
@@ -274,4 +274,24 @@ def test_removed_options_refused_on_host():
         assert rc == -2, name
         msg = lib.maxk_last_error().decode()
         assert "removed in ABI 3" in msg and name.split("_")[0] in msg, msg
+    assert not h.value
+
+
+def test_create_ex_reads_only_the_round1_layout():
+    """maxk_plan_create_ex reads the 120 bytes of its round-1 options layout and no
+    more. A 120-byte buffer followed by bytes that would be invalid options (external_workspace
+    = 7, bwd_flush = 9) is not read past: the call fails on the null graph pointer, not on an
+    option. The same bytes through create_sized with the full size are read and refused."""
+    lib = _lib.lib
+    h = ctypes.c_void_p(0)
+    size = ctypes.sizeof(_lib.PlanOptions)
+    buf = (ctypes.c_int32 * (size // 4))()
+    buf[120 // 4] = 7          # external_workspace
+    buf[124 // 4] = 9          # bwd_flush
+    args = (None, None, None, 10, 10, 100, 256, 16)
+    rc = lib.maxk_plan_create_ex(*args, ctypes.cast(buf, ctypes.c_void_p), None, ctypes.byref(h))
+    assert rc == -1 and "null pointer" in lib.maxk_last_error().decode()
+    rc = lib.maxk_plan_create_sized(*args, ctypes.cast(buf, ctypes.c_void_p), size, None, None,
+                                    ctypes.byref(h))
+    assert rc == -1 and "external_workspace" in lib.maxk_last_error().decode()
     assert not h.value

@@ -1,7 +1,13 @@
 """GPU, BASELINE.json full sizes (synthetic graphs with the datasets' N and E, D=256):
 the top-k bit-exact against the oracle on every row, and the aggregation's parity through
-size-independent properties plus sampled rows/columns checked against the oracle. Cases follow BASELINE.json configs: Reddit SAGE-mean k=16 (the bench
-workload) and k=8/64, ogbn-products SAGE k=32, ogbn-proteins GCN k in {8,16,32,64}.
+size-independent properties plus sampled rows/columns checked against the oracle. Cases follow
+BASELINE.json configs: Reddit SAGE-mean k=16 (the bench workload) and k=8/64, ogbn-products
+SAGE k=32, ogbn-proteins GCN k in {8,16,32,64}.
+
+Two generators per shape: ``synthetic_csr`` (torch's generator, the tests' graphs since round
+1) and ``bench`` = ``graphs.bench_csr`` (the counter-based generator bench.py and
+tools/configs_time.py time since round 4), so the exact graphs behind BENCH's ``value``,
+``k_sweep`` and ``profiles/r0N/configs.json`` are checked in full, at every k of the metric.
 
 * adjoint identity   <A densify(sp), G> == <sp_data, SSpMM(G)>   (float64 reductions)
 * linearity          SpGEMM(2 sp_data) == 2 SpGEMM(sp_data)
@@ -20,29 +26,36 @@ from oracle import oracle
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 D = 256
-CASES = [("reddit", "sage", 16), ("reddit", "sage", 8), ("reddit", "sage", 64),
-         ("ogbn-products", "sage", 32),
-         ("ogbn-proteins", "gcn", 8), ("ogbn-proteins", "gcn", 16),
-         ("ogbn-proteins", "gcn", 32), ("ogbn-proteins", "gcn", 64)]
+CASES = [("reddit", "sage", 16, "csr"), ("reddit", "sage", 8, "csr"),
+         ("reddit", "sage", 64, "csr"),
+         ("ogbn-products", "sage", 32, "csr"),
+         ("ogbn-proteins", "gcn", 8, "csr"), ("ogbn-proteins", "gcn", 16, "csr"),
+         ("ogbn-proteins", "gcn", 32, "csr"), ("ogbn-proteins", "gcn", 64, "csr")] + \
+        [("reddit", "sage", k, "bench") for k in (16, 8, 32, 64)] + \
+        [("ogbn-products", "sage", 32, "bench")] + \
+        [("ogbn-proteins", "gcn", k, "bench") for k in (8, 16, 32, 64)]
 _GRAPHS = {}
 
 
-@pytest.fixture(scope="module", params=CASES, ids=lambda c: f"{c[0]}-{c[1]}-k{c[2]}")
+@pytest.fixture(scope="module", params=CASES, ids=lambda c: f"{c[0]}-{c[1]}-k{c[2]}-{c[3]}")
 def case(request, gpu):
-    name, kind, k = request.param
-    if (name, kind) not in _GRAPHS:
+    name, kind, k, gen = request.param
+    if (name, kind, gen) not in _GRAPHS:
         _GRAPHS.clear()   # one full-size graph resident at a time
         torch.cuda.empty_cache()
         n, e = graphs.DATASETS[name]
-        ptr, idx = graphs.synthetic_csr(n, e, seed=97, device=gpu)
+        if gen == "bench":
+            ptr, idx = graphs.bench_csr(name, device=gpu)
+        else:
+            ptr, idx = graphs.synthetic_csr(n, e, seed=97, device=gpu)
         val = graphs.sage_mean_values(ptr) if kind == "sage" else graphs.gcn_values(ptr, idx)
         h = graphs.features(n, D, seed=97, device=gpu)
         g = graphs.features(n, D, seed=98, device=gpu)
-        _GRAPHS[(name, kind)] = (ptr, idx, val, h, g)
-    ptr, idx, val, h, g = _GRAPHS[(name, kind)]
+        _GRAPHS[(name, kind, gen)] = (ptr, idx, val, h, g)
+    ptr, idx, val, h, g = _GRAPHS[(name, kind, gen)]
     sp_data, sp_index = mk.maxk_forward(h, k, return_index=True)
     mk.clear_plan_cache()
-    return ptr, idx, val, sp_data, sp_index, g, name, k
+    return ptr, idx, val, sp_data, sp_index, g, name, k, gen
 
 
 def test_graph_shape(case):
@@ -52,7 +65,7 @@ def test_graph_shape(case):
 
 
 def test_adjoint_and_linearity(case):
-    ptr, idx, val, sp_data, sp_index, g, _, K = case
+    ptr, idx, val, sp_data, sp_index, g, _, K, _ = case
     N, E = ptr.numel() - 1, idx.numel()
     y, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, N, E, K, D)
     gs = mk.spgemm_backward(ptr, idx, val, g, sp_index, N, E, K, D)
@@ -66,7 +79,7 @@ def test_adjoint_and_linearity(case):
 
 
 def test_sampled_rows_vs_oracle(case):
-    ptr, idx, val, sp_data, sp_index, _, _, K = case
+    ptr, idx, val, sp_data, sp_index, _, _, K, _ = case
     N, E = ptr.numel() - 1, idx.numel()
     y, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, N, E, K, D)
     p = ptr.cpu().numpy()
@@ -90,7 +103,7 @@ def test_sampled_rows_vs_oracle(case):
 
 
 def test_sampled_columns_vs_oracle(case):
-    ptr, idx, val, _, sp_index, g, _, K = case
+    ptr, idx, val, _, sp_index, g, _, K, _ = case
     N, E = ptr.numel() - 1, idx.numel()
     gs = mk.spgemm_backward(ptr, idx, val, g, sp_index, N, E, K, D)
     cols = np.random.RandomState(1).choice(N, 400, replace=False)
@@ -123,17 +136,18 @@ def _close_in_chunks(got, ref, mag, rows=1 << 17):
 def test_every_row_and_column_vs_oracle(case):
     """The whole forward output and the whole backward output at config size against the
     oracle's C/OpenMP restatement (f64 sums; the same bar as the small-graph parity tests)."""
-    ptr, idx, val, sp_data, sp_index, g, _, K = case
+    ptr, idx, val, sp_data, sp_index, g, name, K, gen = case
     N, E = ptr.numel() - 1, idx.numel()
     p, ix, v = ptr.cpu().numpy(), idx.cpu().numpy(), val.cpu().numpy()
     si = sp_index.cpu().numpy()
     y, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, N, E, K, D)
     ref, mag = oracle.spgemm_forward(p, ix, v, sp_data.cpu().numpy(), si, D, with_mag=True)
-    print(f"forward: worst err/bound {_close_in_chunks(y.cpu().numpy(), ref, mag):.3g}")
+    tag = f"{name} k={K} graph={gen} N={N} E={E}"
+    print(f"{tag}: forward: worst err/bound {_close_in_chunks(y.cpu().numpy(), ref, mag):.3g}")
     del y, ref, mag
     gs = mk.spgemm_backward(ptr, idx, val, g, sp_index, N, E, K, D)
     ref, mag = oracle.sspmm_backward(p, ix, v, g.cpu().numpy(), si, with_mag=True)
-    print(f"backward: worst err/bound {_close_in_chunks(gs.cpu().numpy(), ref, mag):.3g}")
+    print(f"{tag}: backward: worst err/bound {_close_in_chunks(gs.cpu().numpy(), ref, mag):.3g}")
 
 
 def test_config3_autograd_step_vs_oracle(gpu):
