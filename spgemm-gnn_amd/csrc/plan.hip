@@ -542,8 +542,8 @@ static int check_options(const maxk_plan_options& o) {
                  "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks) or 3 (two-pass)");
   MAXK_CHECK_REMOVED(o.bwd_algo != 2, "bwd_algo = 2 (column-major)");
   MAXK_CHECK_REMOVED(o.fwd_waves == 0 || o.fwd_waves == 4, "fwd_waves other than 4");
-  MAXK_CHECK_ARG(o.bwd_waves == 0 || o.bwd_waves == 8 || o.bwd_waves == 12,
-                 "maxk_plan_create: bwd_waves must be 0, 8 or 12");
+  MAXK_CHECK_ARG(o.bwd_waves == 0 || o.bwd_waves == 8 || o.bwd_waves == 12 || o.bwd_waves == 16,
+                 "maxk_plan_create: bwd_waves must be 0, 8, 12 or 16");
   MAXK_CHECK_REMOVED((o.fwd_prefetch == 0 || o.fwd_prefetch == 2) &&
                          (o.bwd_prefetch == 0 || o.bwd_prefetch == 2),
                      "fwd_prefetch / bwd_prefetch = 1");
@@ -1294,6 +1294,12 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   }
   p->n_bwd_tasks = (int32_t)btasks.size();
   p->n_bwd_shared = nshared;
+  // One round of tasks (at most one work-group per CU, e.g. an 8-GPU row shard: 256 tasks):
+  // the CU then has only that work-group's waves to hide its gathers, so give it 12 (an
+  // 8-GPU Reddit shard at k = 16: 0.227 -> 0.206 ms; 16 waves profiles/r05/w8_bwd_waves.jsonl)
+  if (o.bwd_waves == 0 && p->n_bwd_tasks > 0 && p->n_bwd_tasks <= cus) p->bwd_waves = 12;
+  // the unroll that actually launches: the 12/16-wave and > 4 GiB shapes run U = 8
+  if (p->bwd_waves != 8 || p->bwd_big) p->bwd_unroll = 8;
   if (!btasks.empty()) {
     PLAN_TRY(hipMalloc(&p->bwd_tasks, sizeof(BwdTask) * btasks.size()));
     PLAN_TRY(hipMemcpyAsync(p->bwd_tasks, btasks.data(), sizeof(BwdTask) * btasks.size(),
