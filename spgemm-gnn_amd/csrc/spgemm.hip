@@ -560,17 +560,82 @@ __global__ void zero_rows_kernel(const int32_t* __restrict__ rows, int nrows, fl
 // grad_out row with buffer loads (32-bit offsets; BIG: grad_out > 4 GiB, the record holds the
 // row index and the gathers are 64-bit addressed). Records past e1 (padding or a
 // neighbouring task's) are loaded and ignored.
-template <int U, int NT, int F, bool Q, bool BIG>
+// Per-lane accumulator update of N sub-steps: lane q adds x[u][0..F) (val already applied) to
+// the F adjacent slots of column cl[u] at accq + cl[u] * KS (accq = accumulators + F q): one
+// ds_read_b128 / b64 of the current values, then one 64-bit compare-and-swap per float pair,
+// all reads first, all CAS next, then retries for the rare pairs another lane or wave changed.
+template <int N, int F>
+__device__ __forceinline__ void bwd_cas_update(unsigned* accq, int KS, const uint32_t (&cl)[N],
+                                               const float (&x)[N][F], const bool (&ok)[N]) {
+  using u64 = unsigned long long;
+  u64 old2[N][F / 2];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    // one ds_read_b128 / b64 (KS % F == 0); a stale value only costs a CAS retry
+    if constexpr (F == 4) {
+      const uint4 o4 = *reinterpret_cast<const uint4*>(accq + cl[u] * KS);
+      old2[u][0] = (u64)o4.x | ((u64)o4.y << 32);
+      old2[u][1] = (u64)o4.z | ((u64)o4.w << 32);
+    } else {
+      const uint2 o2 = *reinterpret_cast<const uint2*>(accq + cl[u] * KS);
+      old2[u][0] = (u64)o2.x | ((u64)o2.y << 32);
+    }
+  }
+  auto addp = [](u64 o, float a0, float a1) -> u64 {
+    const float lo = __uint_as_float((unsigned)o) + a0;
+    const float hi = __uint_as_float((unsigned)(o >> 32)) + a1;
+    return (u64)__float_as_uint(lo) | ((u64)__float_as_uint(hi) << 32);
+  };
+  u64 got2[N][F / 2];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
+#pragma unroll
+    for (int h = 0; h < F / 2; ++h) {
+      got2[u][h] = old2[u][h];
+      if (ok[u]) {
+        u64 expected = old2[u][h];
+        __hip_atomic_compare_exchange_strong(a + h, &expected,
+                                             addp(old2[u][h], x[u][2 * h], x[u][2 * h + 1]),
+                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        got2[u][h] = expected;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
+#pragma unroll
+    for (int h = 0; h < F / 2; ++h) {
+      if (ok[u] && got2[u][h] != old2[u][h]) {
+        u64 cur = got2[u][h];
+        while (true) {
+          u64 expected = cur;
+          __hip_atomic_compare_exchange_strong(a + h, &expected,
+                                               addp(cur, x[u][2 * h], x[u][2 * h + 1]),
+                                               __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (expected == cur) break;
+          cur = expected;
+        }
+      }
+    }
+  }
+}
+
+template <int U, int NT, int F, bool Q, bool BIG, bool HY>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, int D, const uint8_t* __restrict__ sp_index,
     int is, float* __restrict__ grad_sp, int k, int ns, float* __restrict__ slab,
-    const int32_t* __restrict__ corder) {
+    const int32_t* __restrict__ corder, const BwdRun* __restrict__ runs, int dense_waves,
+    int stage_off) {
   static_assert(F == 2 || F == 4, "2 or 4 slots per lane");
   static_assert(!Q || U % 4 == 0, "quad record loads need U % 4 == 0");
   using SelT = std::conditional_t<F == 4, uint32_t, uint16_t>;
-  using u64 = unsigned long long;
   extern __shared__ __align__(16) double bsmem[];
+  __shared__ int s_next[2];  // HY: next dense run / next sparse window of this task
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
   // padding / nothing to add (with the slab flush every piece stores its block, zeros too)
@@ -579,6 +644,10 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const int KS = ns;      // accumulator floats per column
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
+  if (HY && threadIdx.x == 0) {
+    s_next[0] = 0;
+    s_next[1] = 0;
+  }
   SelT* sell = reinterpret_cast<SelT*>(bacc + ((nacc + 3) & ~3));
   {
     uint8_t* sb = reinterpret_cast<uint8_t*>(sell);
@@ -613,7 +682,6 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const int q = lane - slot * L;
   const bool lane_on = slot < EPS;
   constexpr int kWaves = NT / kWave;
-  const int stride = kWaves * EPS * U;
   const __amdgpu_buffer_rsrc_t gr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
   const SelT* selb = sell + q;
@@ -621,7 +689,9 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const uint3* rec3 = reinterpret_cast<const uint3*>(rec);
   const int qq = lane & 3;
 
-  for (int base = t.e0 + wave * EPS * U; base < t.e1; base += stride) {
+  // U sub-steps of EPS edges from `base` (sub-step u, slot s: edge base + u EPS + s, or with Q
+  // lane q of a quad loads sub-step 4j + q's record), gathered from G, up to edge e_end
+  auto gather_window = [&](int base, int e_end) {
     uint32_t go[U], cl[U];
     float v[U];
     bool ok[U];
@@ -631,7 +701,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
       for (int j = 0; j < U / 4; ++j) rq[j] = rec3[base + (4 * j + qq) * EPS + slot];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        ok[u] = lane_on && base + u * EPS + slot < t.e1;
+        ok[u] = lane_on && base + u * EPS + slot < e_end;
         go[u] = quad_pick(rq[u / 4].x, u);
         cl[u] = quad_pick(rq[u / 4].y, u);
         v[u] = __uint_as_float(quad_pick(rq[u / 4].z, u));
@@ -640,7 +710,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = base + u * EPS + slot;
-        ok[u] = lane_on && e < t.e1;
+        ok[u] = lane_on && e < e_end;
         const uint3 r3 = rec3[e];
         go[u] = r3.x;
         cl[u] = r3.y;
@@ -668,61 +738,112 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int i = 0; i < F; ++i) x[u][i] *= v[u];
-    // all reads, then all CAS, then a retry loop for the rare lanes whose CAS lost a race
-    u64 old2[U][F / 2];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      // one ds_read_b128 / b64 (KS % F == 0); a stale value only costs a CAS retry
-      if constexpr (F == 4) {
-        const uint4 o4 = *reinterpret_cast<const uint4*>(accq + cl[u] * KS);
-        old2[u][0] = (u64)o4.x | ((u64)o4.y << 32);
-        old2[u][1] = (u64)o4.z | ((u64)o4.w << 32);
-      } else {
-        const uint2 o2 = *reinterpret_cast<const uint2*>(accq + cl[u] * KS);
-        old2[u][0] = (u64)o2.x | ((u64)o2.y << 32);
-      }
-    }
-    auto addp = [](u64 o, float a0, float a1) -> u64 {
-      const float lo = __uint_as_float((unsigned)o) + a0;
-      const float hi = __uint_as_float((unsigned)(o >> 32)) + a1;
-      return (u64)__float_as_uint(lo) | ((u64)__float_as_uint(hi) << 32);
+    bwd_cas_update<U, F>(accq, KS, cl, x, ok);
+  };
+
+  if constexpr (!HY) {
+    const int stride = kWaves * EPS * U;
+    for (int base = t.e0 + wave * EPS * U; base < t.e1; base += stride) gather_window(base, t.e1);
+  } else {
+    // Dense runs [rb, re) of edges [e0, em) and the rest [em, e1): waves < dense_waves start on
+    // the runs, the others on the rest; both kinds are handed out one at a time (LDS counters,
+    // in stream order) and a wave whose kind is exhausted takes the other one, so the LDS-bound
+    // run work and the texture-bound gathers overlap in every CU.
+    auto grab = [&](int which) -> int {
+      int v = 0;
+      if (lane == 0) v = atomicAdd(&s_next[which], 1);
+      return __builtin_amdgcn_readlane(v, 0);
     };
-    u64 got2[U][F / 2];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
-#pragma unroll
-      for (int h = 0; h < F / 2; ++h) {
-        got2[u][h] = old2[u][h];
-        if (ok[u]) {
-          u64 expected = old2[u][h];
-          __hip_atomic_compare_exchange_strong(a + h, &expected,
-                                               addp(old2[u][h], x[u][2 * h], x[u][2 * h + 1]),
-                                               __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-          got2[u][h] = expected;
-        }
+    auto sparse = [&]() {
+      for (int w = grab(1);; w = grab(1)) {
+        const int base = t.em + w * (EPS * U);
+        if (base >= t.e1) break;
+        gather_window(base, t.e1);
       }
-    }
+    };
+    // Dense runs: wave w < dense_waves takes runs w, w + dense_waves, ... of the task, software
+    // pipelined: while run r is picked, the next run's first two sub-steps of records and its
+    // grad_out row are in flight and the run entry after that is loaded (every load
+    // unconditional, clamped to the last run, so the compiler's in-order wait counts never wait
+    // for a prefetch early). (Batches of 4 runs per iteration, one staged row each: slower,
+    // their empty second sub-steps cost LDS work)
+    auto dense = [&]() {
+      const int nruns = t.re - t.rb;
+      if (wave >= nruns) return;
+      float* row = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(bsmem) + stage_off) +
+                   wave * kMaxDim;
+      const int stride_r = dense_waves;
+      const uint32_t lane_off = 4 * lane < D ? 16u * lane : 0x80000000u;  // past D: reads 0
+      const uint4* runs4 = reinterpret_cast<const uint4*>(runs + t.rb);
+      auto entry = [&](int rr) {  // {g_off, start, len}, wave-uniform
+        const uint4 e = runs4[min(rr, nruns - 1)];
+        return make_uint4(__builtin_amdgcn_readfirstlane(e.x), __builtin_amdgcn_readfirstlane(e.y),
+                          __builtin_amdgcn_readfirstlane(e.z), 0u);
+      };
+      auto row_load = [&](uint32_t g_off) {
+        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(gr, g_off + lane_off, 0, 0));
+      };
+      // one sub-step of EPS edges from base (run [.., rend)): (column, val) of this lane's edge
+      auto rec_load = [&](int base, int rend, int e_first, uint32_t& cl, float& v, bool& ok) {
+        const int e = base + slot;
+        ok = lane_on && e < rend;
+        const uint2 r2 = *reinterpret_cast<const uint2*>(rec + 3 * (size_t)(ok ? e : e_first) + 1);
+        cl = r2.x;
+        v = __uint_as_float(r2.y);
+      };
+      auto pick_update = [&](uint32_t cl, float v, bool ok) {
+        const uint32_t sw = selb[cl * L];
+        uint32_t c1[1] = {cl};
+        bool o1[1] = {ok};
+        float x[1][F];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      u64* a = reinterpret_cast<u64*>(accq + cl[u] * KS);
-#pragma unroll
-      for (int h = 0; h < F / 2; ++h) {
-        if (ok[u] && got2[u][h] != old2[u][h]) {
-          u64 cur = got2[u][h];
-          while (true) {
-            u64 expected = cur;
-            __hip_atomic_compare_exchange_strong(a + h, &expected,
-                                                 addp(cur, x[u][2 * h], x[u][2 * h + 1]),
-                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (expected == cur) break;
-            cur = expected;
-          }
+        for (int i = 0; i < F; ++i) x[0][i] = row[(sw >> (8 * i)) & 0xffu] * v;
+        bwd_cas_update<1, F>(accq, KS, c1, x, o1);
+      };
+      struct Pre {
+        uint32_t cl[2];
+        float v[2];
+        bool ok[2];
+      };
+      auto pre_load = [&](const uint4& e, Pre& p) {
+        const int st = (int)e.y, rend = (int)(e.y + e.z);
+        rec_load(st, rend, st, p.cl[0], p.v[0], p.ok[0]);
+        rec_load(st + EPS, rend, st, p.cl[1], p.v[1], p.ok[1]);
+      };
+      int r = wave;
+      uint4 e0 = entry(r);
+      uint4 e1 = entry(r + stride_r);
+      Pre p0;
+      pre_load(e0, p0);
+      float4 x0 = row_load(e0.x);
+      while (r < nruns) {
+        const uint4 e2 = entry(r + 2 * stride_r);
+        Pre p1;
+        pre_load(e1, p1);
+        const float4 x1 = row_load(e1.x);
+        *reinterpret_cast<float4*>(row + 4 * lane) = x0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pick_update(p0.cl[0], p0.v[0], p0.ok[0]);
+        const int rend = (int)(e0.y + e0.z);
+        if ((int)e0.z > EPS) pick_update(p0.cl[1], p0.v[1], p0.ok[1]);
+        for (int base = (int)e0.y + 2 * EPS; base < rend; base += EPS) {  // runs > 2 EPS edges
+          uint32_t cl;
+          float v;
+          bool ok;
+          rec_load(base, rend, (int)e0.y, cl, v, ok);
+          pick_update(cl, v, ok);
         }
+        e0 = e1;
+        e1 = e2;
+        p0 = p1;
+        x0 = x1;
+        r += stride_r;
       }
-    }
+    };
+    if (wave < dense_waves) dense();
+    sparse();
   }
   __syncthreads();
 
@@ -1414,25 +1535,35 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   const int F = plan->bwd_feats, ns = plan->bwd_ks;
   const int L = ns / F;
   const uint32_t g_bytes = plan->bwd_big ? 0u : (uint32_t)((uint64_t)N * D * 4u);
-  const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, ns);
+  const bool hy = plan->n_bwd_runs > 0 && !plan->bwd_big;
+  // LDS: accumulators + selectors, then (dense runs) one 1 KB staged row per wave
+  const size_t stage_off = (bwd_lds_bytes(plan->bwd_block_cols, ns) + 15) / 16 * 16;
+  const size_t lds = hy ? stage_off + (size_t)plan->bwd_dense_waves * kBwdStageBytes
+                        : bwd_lds_bytes(plan->bwd_block_cols, ns);
   const dim3 grid(plan->n_bwd_tasks);
   const bool Q = L % 4 == 0;  // quad-aligned lane groups: batched record loads
   const int U = plan->bwd_unroll, W = plan->bwd_waves;
-#define BWD_LAUNCH(UU, NT, FF, QQ, BB)                                                      \
+#define BWD_LAUNCH(UU, NT, FF, QQ, BB, HH)                                                  \
   do {                                                                                      \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, FF, QQ, BB>, lds)); \
-    hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, FF, QQ, BB>), grid, dim3(NT), lds, s,     \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, FF, QQ, BB, HH>, lds)); \
+    hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, FF, QQ, BB, HH>), grid, dim3(NT), lds, s, \
                        plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, D, sp_index, is,  \
-                       grad_sp, k, ns, slab, plan->bwd_corder);                             \
+                       grad_sp, k, ns, slab, plan->bwd_corder, plan->bwd_runs,              \
+                       plan->bwd_dense_waves, (int)stage_off);                              \
+  } while (0)
+#define BWD_SHAPES_H(FF, QQ, HH)                                                            \
+  do {                                                                                      \
+    if (W == 16) BWD_LAUNCH(8, 1024, FF, QQ, false, HH);                                    \
+    else if (W == 12) BWD_LAUNCH(8, 768, FF, QQ, false, HH);                                \
+    else if (U == 16) BWD_LAUNCH(16, 512, FF, QQ, false, HH);                               \
+    else if (U == 12) BWD_LAUNCH(12, 512, FF, QQ, false, HH);                               \
+    else BWD_LAUNCH(8, 512, FF, QQ, false, HH);                                             \
   } while (0)
 #define BWD_SHAPES(FF, QQ)                                                                  \
   do {                                                                                      \
-    if (plan->bwd_big) BWD_LAUNCH(8, 512, FF, QQ, true);                                    \
-    else if (W == 16) BWD_LAUNCH(8, 1024, FF, QQ, false);                                   \
-    else if (W == 12) BWD_LAUNCH(8, 768, FF, QQ, false);                                    \
-    else if (U == 16) BWD_LAUNCH(16, 512, FF, QQ, false);                                   \
-    else if (U == 12) BWD_LAUNCH(12, 512, FF, QQ, false);                                   \
-    else BWD_LAUNCH(8, 512, FF, QQ, false);                                                 \
+    if (plan->bwd_big) BWD_LAUNCH(8, 512, FF, QQ, true, false);                             \
+    else if (hy) BWD_SHAPES_H(FF, QQ, true);                                                \
+    else BWD_SHAPES_H(FF, QQ, false);                                                       \
   } while (0)
   if (F == 4) {
     if (Q) BWD_SHAPES(4, true);
@@ -1441,6 +1572,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     if (Q) BWD_SHAPES(2, true);
     else BWD_SHAPES(2, false);
   }
+#undef BWD_SHAPES_H
 #undef BWD_SHAPES
 #undef BWD_LAUNCH
   MAXK_LAUNCH_CHECK("sspmm_bwd launch");

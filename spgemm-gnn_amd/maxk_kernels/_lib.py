@@ -114,6 +114,9 @@ class PlanOptions(ctypes.Structure):
         ("col_order", _i32),
         ("bwd_tp_chunks", _i32),
         ("bwd_row_order", _i32),
+        # round 5
+        ("bwd_dense_min", _i32),
+        ("bwd_dense_waves", _i32),
     ]
 
 
@@ -147,6 +150,10 @@ class PlanInfo(ctypes.Structure):
         ("bwd_tp_chunks", _i32),
         ("bwd_row_order", _i32),
         ("bwd_workspace_peak", _i64),
+        # round 5
+        ("bwd_dense_edges", _i64),
+        ("bwd_dense_runs", _i32),
+        ("bwd_dense_min", _i32),
     ]
 
     def as_dict(self):

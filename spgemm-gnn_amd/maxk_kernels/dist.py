@@ -24,6 +24,14 @@ first 8 bytes of that record (``maxk_cbsr_stats``: two words), the gathered tabl
 pair per rank and the forward reads those W pairs (``maxk_spgemm_forward_ex``) instead of
 scanning the whole table.
 
+The spare rows (``RowPartition.stats_position``) are therefore NOT CBSR data: their first two
+"values" are statistics words. No edge reads them, so the shard's own forward and backward are
+unaffected, but a pass over the whole gathered table would take those bit patterns for values:
+``cbsr_stats(shard.table_data, ...)`` or a ``GraphPlan.forward`` on the shard's tables without
+``stats=`` (its own statistics pass would count the spare rows, coarsening the fixed-point
+scale or falling back to f64). Use ``ShardedAggregation.forward`` / ``compute_forward`` (they
+pass the per-rank pairs) and ``unpad_table`` (node rows only) for such passes.
+
 Bytes exchanged per step are 5kN (all-gather) + 4kN (reduce-scatter), i.e. 18.6 MB + 14.9 MB
 for Reddit at k=16, against 238 MB for all-gathering dense features. Round 3's two
 all-gathers (values, selectors), column phases and local-columns-first split are gone: the
@@ -144,6 +152,7 @@ class ShardedAggregation:
         self.send_rec = torch.zeros((part.block_rows, rb), dtype=torch.uint8, device=dev)
         self.table_rec = torch.zeros((part.padded_rows, rb), dtype=torch.uint8, device=dev)
         self.send_data, self.send_index = record_views(self.send_rec, k)
+        # rows stats_position(q) of these views are the spare statistics records, not CBSR data
         self.table_data, self.table_index = record_views(self.table_rec, k)
         self.grad_table = torch.empty((part.padded_rows, k), dtype=torch.float32, device=dev)
         self.grad_local = torch.empty((part.block_rows, k), dtype=torch.float32, device=dev)

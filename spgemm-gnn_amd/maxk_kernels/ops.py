@@ -246,7 +246,9 @@ class GraphPlan:
         fixed-point statistics covering the table instead of a pass over it, either an int32
         [n, 2] tensor of :func:`cbsr_stats` pairs or ``(tensor, n, stride)`` with pair i at
         32-bit word i * stride of the tensor's storage (the multi-GPU path keeps one pair
-        per rank in a spare row of the gathered table)."""
+        per rank in a spare row of the gathered table). Without ``stats`` the call scans
+        every row of the tables, so each row must be CBSR data: a ShardedAggregation's
+        gathered table is not (its spare rows hold those pairs), pass its ``stats``."""
         ptr, idx, val = self._refs
         if out is None:
             if accumulate:

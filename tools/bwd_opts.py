@@ -55,7 +55,9 @@ def main():
         t = sorted(times[i])
         print(json.dumps({"dataset": args.dataset, "k": args.k, "opts": o,
                           "bwd_ms": round(t[len(t) // 2], 4), "bwd_ms_all": [round(x, 4) for x in times[i]],
-                          "tasks": plans[i].info()["bwd_tasks"], "max_rel_dev": dev_max}), flush=True)
+                          "tasks": plans[i].info()["bwd_tasks"], "max_rel_dev": dev_max,
+                          "dense_edges": plans[i].info().get("bwd_dense_edges"),
+                          "dense_runs": plans[i].info().get("bwd_dense_runs")}), flush=True)
 
 
 if __name__ == "__main__":
