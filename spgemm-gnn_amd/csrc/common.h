@@ -131,30 +131,9 @@ struct BwdTask {
   int32_t chunk;  // piece index within its block (0 .. pieces - 1)
   int32_t slab;   // slab flush: float offset of this piece's [C][k] slab region; -1: piece
                   // 0 (stores straight into grad_sp)
-  // dense runs (plan->bwd_dense_min): [e0, em) holds the task's edges that belong to runs of
-  // >= bwd_dense_min edges on one grad_out row, run by run (runs [rb, re) of plan->bwd_runs);
-  // [em, e1) the rest, in stream order. em = e0 and rb = re without dense runs
-  int32_t em;
-  int32_t rb;
-  int32_t re;
-  int32_t pad;
 };
-static_assert(sizeof(BwdTask) == 48, "BwdTask is 3 x dwordx4");
+static_assert(sizeof(BwdTask) == 32, "BwdTask is 2 x dwordx4");
 
-// A dense run of the column-block backward: `len` consecutive edges (from position `start`
-// of the block stream) of one grad_out row, whose byte offset is g_off; the kernel stages the
-// row in LDS once and picks the run's selected features there (sspmm_bwd4_kernel).
-struct BwdRun {
-  uint32_t g_off;
-  int32_t start;
-  int32_t len;
-  int32_t pad;
-};
-static_assert(sizeof(BwdRun) == 16, "BwdRun is one dwordx4");
-// LDS staging per dense-run wave: one 1 KB grad_out row (the wave's LDS operations are in
-// order, so the next run's row is written after the previous run's picks were issued)
-constexpr int kBwdStageBytes = kMaxDim * 4;
-constexpr int kBwdDenseMinAuto = 8;  // auto bwd_dense_min
 
 __device__ __forceinline__ void lds_add(double* p, double v) {
   // ds_add_f64 (no return).
@@ -256,11 +235,8 @@ struct maxk_plan {
   int64_t fwd_ws_bytes = 0;
   int64_t bwd_ws_bytes = 0;
   int32_t bwd_row_order = 1;     // rows in the block streams: 1 ascending, 2 scattered
-  // dense runs of the column blocks (0: none): runs of >= bwd_dense_min edges on one grad_out
-  // row within a task are staged in LDS by bwd_dense_waves of the work-group's waves
-  int32_t bwd_dense_min = 0;
-  int32_t bwd_dense_waves = 0;
-  maxk::BwdRun* bwd_runs = nullptr;
-  int32_t n_bwd_runs = 0;
-  int64_t bwd_dense_edges = 0;
+  // windows of the forward / column-block backward waves: 1 static interleave, 2 handed out
+  // by a per-work-group LDS counter (maxk_plan_options.fwd_handout / bwd_handout)
+  int32_t fwd_handout = 1;
+  int32_t bwd_handout = 1;
 };

@@ -341,98 +341,6 @@ __global__ void iota_kernel(int n, int32_t* __restrict__ out) {
 }
 
 
-// ---- dense runs of the column-block streams (plan->bwd_dense_min) ---------------------------
-// A run = consecutive positions of one task range with the same destination row. flag[i] = 1
-// where a run starts: a new row, or a task range start (ranges are disjoint and cover [0, E);
-// a block's first position is a range start).
-__global__ void run_flags_kernel(const int32_t* __restrict__ brow, int64_t E,
-                                 uint32_t* __restrict__ flag) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
-       i += (int64_t)gridDim.x * blockDim.x)
-    flag[i] = (i == 0 || brow[i] != brow[i - 1]) ? 1u : 0u;
-}
-
-__global__ void mark_starts_kernel(const int2* __restrict__ ranges, int nr,
-                                   uint32_t* __restrict__ flag) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < nr && ranges[t].x < ranges[t].y) flag[ranges[t].x] = 1u;
-}
-
-// rstart[r] = first position of run r (runid1 = inclusive scan of flag, runs numbered from 1);
-// rstart[nruns] = E
-__global__ void run_starts_kernel(const uint32_t* __restrict__ flag,
-                                  const uint32_t* __restrict__ runid1, int64_t E,
-                                  int32_t* __restrict__ rstart) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    if (flag[i]) rstart[runid1[i] - 1] = (int32_t)i;
-    if (i == E - 1) rstart[runid1[i]] = (int32_t)E;
-  }
-}
-
-// per position: 1 if its run is dense (>= M edges); per run: the same flag (rdense)
-__global__ void dense_flags_kernel(const uint32_t* __restrict__ runid1,
-                                   const int32_t* __restrict__ rstart, int64_t E, int M,
-                                   uint32_t* __restrict__ dflag, uint32_t* __restrict__ rdense) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t r = runid1[i] - 1;
-    const bool d = rstart[r + 1] - rstart[r] >= M;
-    dflag[i] = d ? 1u : 0u;
-    if (rstart[r] == i) rdense[r] = d ? 1u : 0u;
-  }
-}
-
-// Per task range t: dense edge count, and its dense runs [rb, re) in the compacted run list
-// (dx: exclusive scan of dflag, E + 1 entries; rdx: exclusive scan of rdense, nruns + 1).
-__global__ void range_dense_kernel(const int2* __restrict__ ranges, int nr,
-                                   const uint32_t* __restrict__ dx,
-                                   const uint32_t* __restrict__ runid1,
-                                   const uint32_t* __restrict__ rdx, int4* __restrict__ out) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nr) return;
-  const int2 r = ranges[t];
-  if (r.x >= r.y) {
-    out[t] = make_int4(0, 0, 0, 0);
-    return;
-  }
-  out[t] = make_int4((int)(dx[r.y] - dx[r.x]), (int)rdx[runid1[r.x] - 1], (int)rdx[runid1[r.y - 1]], 0);
-}
-
-// New position of every edge: inside its task range, the dense-run edges first (stream order),
-// then the others (stream order). Permutes perm / brow / bcol and writes the dense-run table
-// {row byte offset, new start, length}.
-__global__ void dense_reorder_kernel(const int2* __restrict__ ranges, int nr,
-                                     const int4* __restrict__ rd, const uint32_t* __restrict__ dflag,
-                                     const uint32_t* __restrict__ dx, const uint32_t* __restrict__ flag,
-                                     const uint32_t* __restrict__ runid1,
-                                     const int32_t* __restrict__ rstart,
-                                     const uint32_t* __restrict__ rdx, int64_t E, int D,
-                                     const int32_t* __restrict__ perm, const int32_t* __restrict__ brow,
-                                     const int32_t* __restrict__ bcol, int32_t* __restrict__ perm2,
-                                     int32_t* __restrict__ brow2, int32_t* __restrict__ bcol2,
-                                     BwdRun* __restrict__ runs) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    int lo = 0, hi = nr - 1;  // the range holding i: the last one with start <= i
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (ranges[mid].x <= i) lo = mid; else hi = mid - 1;
-    }
-    const int64_t e0 = ranges[lo].x;
-    const int64_t before = (int64_t)dx[i] - dx[e0];  // dense edges of the range before i
-    const int64_t np = dflag[i] ? e0 + before : e0 + rd[lo].x + (i - e0) - before;
-    perm2[np] = perm[i];
-    brow2[np] = brow[i];
-    bcol2[np] = bcol[i];
-    if (flag[i] && dflag[i]) {
-      const uint32_t r = runid1[i] - 1;
-      runs[rdx[r]] = BwdRun{(uint32_t)brow[i] * (uint32_t)D * 4u, (int32_t)np,
-                            rstart[r + 1] - rstart[r], 0};
-    }
-  }
-}
-
 static void dfree(void* q) { if (q) (void)hipFree(q); }
 
 static int grid_for(int64_t n, int threads) {
@@ -460,7 +368,6 @@ static void free_plan(maxk_plan* p) {
   dfree(p->bwd_combine);
   dfree(p->bwd_colptr2);
   dfree(p->bwd_corder);
-  dfree(p->bwd_runs);
   delete p;
 }
 
@@ -638,8 +545,8 @@ static int check_options(const maxk_plan_options& o) {
   MAXK_CHECK_REMOVED(o.fwd_waves == 0 || o.fwd_waves == 4, "fwd_waves other than 4");
   MAXK_CHECK_ARG(o.bwd_waves == 0 || o.bwd_waves == 8 || o.bwd_waves == 12 || o.bwd_waves == 16,
                  "maxk_plan_create: bwd_waves must be 0, 8, 12 or 16");
-  MAXK_CHECK_ARG(o.bwd_dense_waves >= 0 && o.bwd_dense_waves <= 16,
-                 "maxk_plan_create: bwd_dense_waves must be in [0, 16]");
+  MAXK_CHECK_ARG(o.fwd_handout >= 0 && o.fwd_handout <= 2 && o.bwd_handout >= 0 && o.bwd_handout <= 2,
+                 "maxk_plan_create: fwd_handout / bwd_handout must be 0, 1 or 2");
   MAXK_CHECK_REMOVED((o.fwd_prefetch == 0 || o.fwd_prefetch == 2) &&
                          (o.bwd_prefetch == 0 || o.bwd_prefetch == 2),
                      "fwd_prefetch / bwd_prefetch = 1");
@@ -769,16 +676,8 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   p->bwd_unroll = o.bwd_unroll ? o.bwd_unroll : (F == 2 ? 12 : 8);
   p->bwd_waves = o.bwd_waves ? o.bwd_waves : (k >= 32 ? 12 : 8);
   p->bwd_big = (uint64_t)N * (uint64_t)D * 4u > 0xffffffffull;  // 32-bit buffer offsets
-  // dense runs (column blocks): the LDS keeps room to stage up to 8 waves' rows;
-  // not with grad_out > 4 GiB (32-bit row offsets in the run table), D % 4 != 0 (16-B row
-  // loads) or an LDS budget too small for the staging
-  const int stage_reserve = (o.bwd_dense_waves ? o.bwd_dense_waves : 4) * kBwdStageBytes;
-  const int dense_min = (o.bwd_dense_min < 0 || p->bwd_big || D % 4 != 0 ||
-                         lds_budget - 16 - stage_reserve < 40 * 5 * p->bwd_ks)
-                            ? 0
-                            : (o.bwd_dense_min > 0 ? o.bwd_dense_min : kBwdDenseMinAuto);
   // bytes of LDS per column: ks f32 accumulators + ks staged selector bytes
-  int C = std::max(1, (lds_budget - 16 - (dense_min ? stage_reserve : 0)) / (5 * p->bwd_ks));
+  int C = std::max(1, (lds_budget - 16) / (5 * p->bwd_ks));
   C = std::min(C, std::max(NC, 1));
 
   int32_t* row_of = nullptr;
@@ -1363,7 +1262,6 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
           t.chunk = piece;
           t.slab = (slab_base[b] >= 0 && piece > 0)
                        ? (int32_t)(slab_base[b] + (int64_t)(piece - 1) * C * k) : -1;
-          t.em = t.e0;  // no dense runs until the dense-run pass below
           btasks.push_back(t);
         }
       }
@@ -1376,110 +1274,6 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
                               hipMemcpyHostToDevice, s));
       PLAN_TRY(hipStreamSynchronize(s));
       p->device_bytes += sizeof(int4) * comb.size();
-    }
-  }
-  // Dense runs: within every task range, the runs of >= dense_min edges on one grad_out row go
-  // to the front of the range (run by run, the block's row order kept), the other edges after
-  // them; the kernel stages a dense run's row in LDS once while other waves gather the sparse
-  // edges. Runs are cut at task ranges, so a run never spans two work-groups.
-  if (dense_min > 0 && !btasks.empty() && E > 0) {
-    std::vector<int2> ranges;
-    for (const BwdTask& t : btasks)
-      if (t.group == 0 && t.e1 > t.e0) ranges.push_back(make_int2(t.e0, t.e1));
-    std::sort(ranges.begin(), ranges.end(), [](const int2& a, const int2& b) { return a.x < b.x; });
-    const int nr = (int)ranges.size();
-    int2* d_ranges = nullptr;
-    int4* d_rd = nullptr;
-    uint32_t *flag = nullptr, *runid1 = nullptr, *dflag = nullptr, *dx = nullptr, *rdense = nullptr,
-             *rdx = nullptr;
-    int32_t *rstart = nullptr, *perm2 = nullptr, *brow2 = nullptr, *bcol2 = nullptr;
-    std::vector<int4> rd(nr);
-    uint32_t nruns = 0, ndense = 0, dedges = 0;
-    BwdRun* runs = nullptr;
-    const hipError_t de = [&]() -> hipError_t {
-      hipError_t e = hipMalloc(&d_ranges, sizeof(int2) * nr);
-      if (e == hipSuccess) e = hipMalloc(&d_rd, sizeof(int4) * nr);
-      if (e == hipSuccess) e = hipMalloc(&flag, sizeof(uint32_t) * E);
-      if (e == hipSuccess) e = hipMalloc(&runid1, sizeof(uint32_t) * E);
-      if (e == hipSuccess) e = hipMalloc(&dflag, sizeof(uint32_t) * (E + 1));
-      if (e == hipSuccess) e = hipMalloc(&dx, sizeof(uint32_t) * (E + 1));
-      if (e == hipSuccess) e = hipMalloc(&rstart, sizeof(int32_t) * (E + 1));
-      if (e == hipSuccess) e = hipMalloc(&rdense, sizeof(uint32_t) * (E + 1));
-      if (e == hipSuccess) e = hipMalloc(&rdx, sizeof(uint32_t) * (E + 1));
-      if (e == hipSuccess) e = hipMemcpyAsync(d_ranges, ranges.data(), sizeof(int2) * nr,
-                                              hipMemcpyHostToDevice, s);
-      if (e != hipSuccess) return e;
-      const int g = grid_for(E, 256);
-      hipLaunchKernelGGL(run_flags_kernel, dim3(g), dim3(256), 0, s, brow, E, flag);
-      hipLaunchKernelGGL(mark_starts_kernel, dim3((nr + 255) / 256), dim3(256), 0, s, d_ranges, nr, flag);
-      size_t tb = 0;
-      e = hipcub::DeviceScan::InclusiveSum(nullptr, tb, flag, runid1, (int)E, s);
-      if (e == hipSuccess) { dfree(temp); temp = nullptr; e = hipMalloc(&temp, tb); }
-      if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(temp, tb, flag, runid1, (int)E, s);
-      if (e == hipSuccess) e = hipMemcpyAsync(&nruns, runid1 + E - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(run_starts_kernel, dim3(g), dim3(256), 0, s, flag, runid1, E, rstart);
-      e = hipMemsetAsync(dflag + E, 0, sizeof(uint32_t), s);
-      if (e == hipSuccess) e = hipMemsetAsync(rdense + nruns, 0, sizeof(uint32_t), s);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(dense_flags_kernel, dim3(g), dim3(256), 0, s, runid1, rstart, E, dense_min,
-                         dflag, rdense);
-      size_t tb2 = 0, tb3 = 0;
-      e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, dflag, dx, (int)(E + 1), s);
-      if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, rdense, rdx, (int)(nruns + 1), s);
-      if (e == hipSuccess && std::max(tb2, tb3) > tb) {
-        dfree(temp);
-        temp = nullptr;
-        tb = std::max(tb2, tb3);
-        e = hipMalloc(&temp, tb);
-      }
-      if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, tb2, dflag, dx, (int)(E + 1), s);
-      if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(temp, tb3, rdense, rdx, (int)(nruns + 1), s);
-      if (e == hipSuccess) e = hipMemcpyAsync(&dedges, dx + E, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-      if (e == hipSuccess) e = hipMemcpyAsync(&ndense, rdx + nruns, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(range_dense_kernel, dim3((nr + 255) / 256), dim3(256), 0, s, d_ranges, nr,
-                         dx, runid1, rdx, d_rd);
-      e = hipMemcpyAsync(rd.data(), d_rd, sizeof(int4) * nr, hipMemcpyDeviceToHost, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
-      if (e != hipSuccess || ndense == 0) return e;
-      e = hipMalloc(&runs, sizeof(BwdRun) * ndense);
-      if (e == hipSuccess) e = hipMalloc(&perm2, sizeof(int32_t) * E);
-      if (e == hipSuccess) e = hipMalloc(&brow2, sizeof(int32_t) * E);
-      if (e == hipSuccess) e = hipMalloc(&bcol2, sizeof(int32_t) * E);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(dense_reorder_kernel, dim3(g), dim3(256), 0, s, d_ranges, nr, d_rd, dflag,
-                         dx, flag, runid1, rstart, rdx, E, D, p->bwd_perm, brow, bcol, perm2, brow2,
-                         bcol2, runs);
-      e = hipGetLastError();
-      return e == hipSuccess ? hipStreamSynchronize(s) : e;
-    }();
-    dfree(d_ranges); dfree(d_rd); dfree(flag); dfree(runid1); dfree(dflag); dfree(dx);
-    dfree(rstart); dfree(rdense); dfree(rdx);
-    if (de != hipSuccess) {
-      dfree(runs); dfree(perm2); dfree(brow2); dfree(bcol2);
-      PLAN_TRY(de);
-    }
-    if (ndense > 0) {
-      std::swap(p->bwd_perm, perm2);
-      std::swap(brow, brow2);
-      std::swap(bcol, bcol2);
-      dfree(perm2); dfree(brow2); dfree(bcol2);
-      p->bwd_runs = runs;
-      p->n_bwd_runs = (int32_t)ndense;
-      p->bwd_dense_edges = dedges;
-      p->bwd_dense_min = dense_min;
-      p->device_bytes += sizeof(BwdRun) * (int64_t)ndense;
-      for (BwdTask& t : btasks) {
-        if (t.e1 <= t.e0) continue;
-        const auto it = std::lower_bound(ranges.begin(), ranges.end(), t.e0,
-                                         [](const int2& a, int32_t v) { return a.x < v; });
-        const int4 r = rd[it - ranges.begin()];
-        t.em = t.e0 + r.x;
-        t.rb = r.y;
-        t.re = r.z;
-      }
     }
   }
   // default on with one slot group (Reddit k = 16: 1.665 -> 1.626 ms, an 8-GPU row shard
@@ -1509,9 +1303,10 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   if (o.bwd_waves == 0 && p->n_bwd_tasks > 0 && p->n_bwd_tasks <= cus) p->bwd_waves = 12;
   // the unroll that actually launches: the 12/16-wave and > 4 GiB shapes run U = 8
   if (p->bwd_waves != 8 || p->bwd_big) p->bwd_unroll = 8;
-  // dense-run waves (their staging was reserved above: 4 by default)
-  p->bwd_dense_waves = p->n_bwd_runs == 0 ? 0
-                       : std::min(p->bwd_waves - 1, o.bwd_dense_waves ? o.bwd_dense_waves : 4);
+  // window hand-out: an LDS counter for the backward when work-groups run in
+  // more than one round, the static interleave otherwise and for the forward
+  p->bwd_handout = o.bwd_handout ? o.bwd_handout : (p->n_bwd_tasks > cus ? 2 : 1);
+  p->fwd_handout = o.fwd_handout ? o.fwd_handout : 1;
   if (!btasks.empty()) {
     PLAN_TRY(hipMalloc(&p->bwd_tasks, sizeof(BwdTask) * btasks.size()));
     PLAN_TRY(hipMemcpyAsync(p->bwd_tasks, btasks.data(), sizeof(BwdTask) * btasks.size(),
@@ -1603,9 +1398,8 @@ extern "C" int maxk_plan_get_info_sized(const maxk_plan* p, maxk_plan_info* out,
   info.bwd_tp_chunks = p->bwd_twopass ? p->bwd_tp_chunks : 1;
   info.bwd_row_order = p->bwd_row_order;
   info.bwd_workspace_peak = p->bwd_ws_bytes;
-  info.bwd_dense_edges = p->bwd_dense_edges;
-  info.bwd_dense_runs = p->n_bwd_runs;
-  info.bwd_dense_min = p->n_bwd_runs ? p->bwd_dense_min : 0;
+  info.fwd_handout = p->fwd_handout;
+  info.bwd_handout = p->bwd_handout;
   std::memcpy(out, &info, (size_t)std::min<int64_t>(info_bytes, (int64_t)sizeof(maxk_plan_info)));
   return MAXK_OK;
 }

@@ -329,8 +329,9 @@ __global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
 // (Batching the selector words the same way, 64 scattered records per instruction, ran k = 16
 // 1.10 -> 1.48 ms: only contiguous loads gain from fewer instructions.)
 template <class A, int FL>
-__device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, int wave,
-                                           int nwaves, int EPS, int slot, int l0, bool lane_on,
+__device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, int* ctr,
+                                           int wave, int nwaves, int EPS, int slot, int l0,
+                                           bool lane_on,
                                            const uint2* __restrict__ cv,
                                            const uint8_t* __restrict__ rec, int rec_bytes,
                                            const uint8_t* __restrict__ seltab, int ss, int D,
@@ -340,9 +341,18 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
   constexpr bool EM = (FL & kFwdFlagQuad) != 0;
   const int last = e1 - 1;
-  const int stride = nwaves * EPS * U;
   const int qq = threadIdx.x & 3;
-  for (int base = e0 + wave * EPS * U; base < e1; base += stride) {
+  // window i of this wave: wave + i * nwaves (static), or (ctr != nullptr: plan->fwd_handout
+  // 2) the next one of the task's LDS counter *ctr, handed out in order one at a time
+  for (int i = 0;; ++i) {
+    int wi = wave + i * nwaves;
+    if (ctr) {
+      int c = 0;
+      if ((threadIdx.x & (kWave - 1)) == 0) c = atomicAdd(ctr, 1);
+      wi = __builtin_amdgcn_readlane(c, 0);
+    }
+    const int base = e0 + wi * (EPS * U);
+    if (base >= e1) break;
     uint32_t cw[U];
     float v[U];
     bool ok[U];
@@ -423,11 +433,16 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
     const uint8_t* __restrict__ sp_index, const uint8_t* __restrict__ rec, int rec_bytes,
     float* __restrict__ out, int D, int k, int rot_ticks, const uint8_t* __restrict__ seltab,
     int ss, int ds, int accum, const int2* __restrict__ fix_tab,
-    const uint32_t* __restrict__ xstat, int xs_n, int xs_stride, int xs_off2) {
+    const uint32_t* __restrict__ xstat, int xs_n, int xs_stride, int xs_off2, int handout) {
   extern __shared__ __align__(16) double smem_d[];
   double* acc = smem_d;
   unsigned long long* acc64 = reinterpret_cast<unsigned long long*>(smem_d);
   __shared__ int s_w0;
+  __shared__ int s_win[2];  // window counters of the task's two sweeps (fwd_edges4)
+  if (threadIdx.x == 0) {
+    s_win[0] = 0;
+    s_win[1] = 0;
+  }
   const int ti = blockIdx.x;
   FwdTask t = tasks[ti];
   t.e0 = phase_off[ti * (phases + 1)];
@@ -477,13 +492,15 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   if constexpr (VEC == 4) {
     auto sweep = [&](auto* a, auto tag) {
       using AA = decltype(tag);
+      int* c0 = handout ? &s_win[0] : nullptr;
+      int* c1 = handout ? &s_win[1] : nullptr;
       if (emid >= 0) {
-        fwd_edges4<AA, FL>(a, emid, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+        fwd_edges4<AA, FL>(a, emid, t.e1, c0, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, seltab, ss, DS, k, fsc);
-        fwd_edges4<AA, FL>(a, t.e0, emid, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+        fwd_edges4<AA, FL>(a, t.e0, emid, c1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, seltab, ss, DS, k, fsc);
       } else {
-        fwd_edges4<AA, FL>(a, t.e0, t.e1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+        fwd_edges4<AA, FL>(a, t.e0, t.e1, c0, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, seltab, ss, DS, k, fsc);
       }
     };
@@ -624,18 +641,17 @@ __device__ __forceinline__ void bwd_cas_update(unsigned* accq, int KS, const uin
   }
 }
 
-template <int U, int NT, int F, bool Q, bool BIG, bool HY>
+template <int U, int NT, int F, bool Q, bool BIG>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
     const float* __restrict__ G, uint32_t g_bytes, int D, const uint8_t* __restrict__ sp_index,
     int is, float* __restrict__ grad_sp, int k, int ns, float* __restrict__ slab,
-    const int32_t* __restrict__ corder, const BwdRun* __restrict__ runs, int dense_waves,
-    int stage_off) {
+    const int32_t* __restrict__ corder, int handout) {
   static_assert(F == 2 || F == 4, "2 or 4 slots per lane");
   static_assert(!Q || U % 4 == 0, "quad record loads need U % 4 == 0");
   using SelT = std::conditional_t<F == 4, uint32_t, uint16_t>;
   extern __shared__ __align__(16) double bsmem[];
-  __shared__ int s_next[2];  // HY: next dense run / next sparse window of this task
+  __shared__ int s_next;  // next window of the task's edge stream to hand out
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
   // padding / nothing to add (with the slab flush every piece stores its block, zeros too)
@@ -644,10 +660,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   const int KS = ns;      // accumulator floats per column
   const int nacc = t.ncols * KS;
   for (int i = threadIdx.x; i < nacc; i += NT) bacc[i] = 0.f;
-  if (HY && threadIdx.x == 0) {
-    s_next[0] = 0;
-    s_next[1] = 0;
-  }
+  if (threadIdx.x == 0) s_next = 0;
   SelT* sell = reinterpret_cast<SelT*>(bacc + ((nacc + 3) & ~3));
   {
     uint8_t* sb = reinterpret_cast<uint8_t*>(sell);
@@ -677,11 +690,9 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
 
   const int EPS = kWave / L;
   const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
   const int slot = lane / L;
   const int q = lane - slot * L;
   const bool lane_on = slot < EPS;
-  constexpr int kWaves = NT / kWave;
   const __amdgpu_buffer_rsrc_t gr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), (short)0, (int)g_bytes, 0x00020000);
   const SelT* selb = sell + q;
@@ -741,109 +752,22 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     bwd_cas_update<U, F>(accq, KS, cl, x, ok);
   };
 
-  if constexpr (!HY) {
-    const int stride = kWaves * EPS * U;
-    for (int base = t.e0 + wave * EPS * U; base < t.e1; base += stride) gather_window(base, t.e1);
-  } else {
-    // Dense runs [rb, re) of edges [e0, em) and the rest [em, e1): waves < dense_waves start on
-    // the runs, the others on the rest; both kinds are handed out one at a time (LDS counters,
-    // in stream order) and a wave whose kind is exhausted takes the other one, so the LDS-bound
-    // run work and the texture-bound gathers overlap in every CU.
-    auto grab = [&](int which) -> int {
-      int v = 0;
-      if (lane == 0) v = atomicAdd(&s_next[which], 1);
-      return __builtin_amdgcn_readlane(v, 0);
-    };
-    auto sparse = [&]() {
-      for (int w = grab(1);; w = grab(1)) {
-        const int base = t.em + w * (EPS * U);
-        if (base >= t.e1) break;
-        gather_window(base, t.e1);
-      }
-    };
-    // Dense runs: wave w < dense_waves takes runs w, w + dense_waves, ... of the task, software
-    // pipelined: while run r is picked, the next run's first two sub-steps of records and its
-    // grad_out row are in flight and the run entry after that is loaded (every load
-    // unconditional, clamped to the last run, so the compiler's in-order wait counts never wait
-    // for a prefetch early). (Batches of 4 runs per iteration, one staged row each: slower,
-    // their empty second sub-steps cost LDS work)
-    auto dense = [&]() {
-      const int nruns = t.re - t.rb;
-      if (wave >= nruns) return;
-      float* row = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(bsmem) + stage_off) +
-                   wave * kMaxDim;
-      const int stride_r = dense_waves;
-      const uint32_t lane_off = 4 * lane < D ? 16u * lane : 0x80000000u;  // past D: reads 0
-      const uint4* runs4 = reinterpret_cast<const uint4*>(runs + t.rb);
-      auto entry = [&](int rr) {  // {g_off, start, len}, wave-uniform
-        const uint4 e = runs4[min(rr, nruns - 1)];
-        return make_uint4(__builtin_amdgcn_readfirstlane(e.x), __builtin_amdgcn_readfirstlane(e.y),
-                          __builtin_amdgcn_readfirstlane(e.z), 0u);
-      };
-      auto row_load = [&](uint32_t g_off) {
-        return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(gr, g_off + lane_off, 0, 0));
-      };
-      // one sub-step of EPS edges from base (run [.., rend)): (column, val) of this lane's edge
-      auto rec_load = [&](int base, int rend, int e_first, uint32_t& cl, float& v, bool& ok) {
-        const int e = base + slot;
-        ok = lane_on && e < rend;
-        const uint2 r2 = *reinterpret_cast<const uint2*>(rec + 3 * (size_t)(ok ? e : e_first) + 1);
-        cl = r2.x;
-        v = __uint_as_float(r2.y);
-      };
-      auto pick_update = [&](uint32_t cl, float v, bool ok) {
-        const uint32_t sw = selb[cl * L];
-        uint32_t c1[1] = {cl};
-        bool o1[1] = {ok};
-        float x[1][F];
-#pragma unroll
-        for (int i = 0; i < F; ++i) x[0][i] = row[(sw >> (8 * i)) & 0xffu] * v;
-        bwd_cas_update<1, F>(accq, KS, c1, x, o1);
-      };
-      struct Pre {
-        uint32_t cl[2];
-        float v[2];
-        bool ok[2];
-      };
-      auto pre_load = [&](const uint4& e, Pre& p) {
-        const int st = (int)e.y, rend = (int)(e.y + e.z);
-        rec_load(st, rend, st, p.cl[0], p.v[0], p.ok[0]);
-        rec_load(st + EPS, rend, st, p.cl[1], p.v[1], p.ok[1]);
-      };
-      int r = wave;
-      uint4 e0 = entry(r);
-      uint4 e1 = entry(r + stride_r);
-      Pre p0;
-      pre_load(e0, p0);
-      float4 x0 = row_load(e0.x);
-      while (r < nruns) {
-        const uint4 e2 = entry(r + 2 * stride_r);
-        Pre p1;
-        pre_load(e1, p1);
-        const float4 x1 = row_load(e1.x);
-        *reinterpret_cast<float4*>(row + 4 * lane) = x0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        pick_update(p0.cl[0], p0.v[0], p0.ok[0]);
-        const int rend = (int)(e0.y + e0.z);
-        if ((int)e0.z > EPS) pick_update(p0.cl[1], p0.v[1], p0.ok[1]);
-        for (int base = (int)e0.y + 2 * EPS; base < rend; base += EPS) {  // runs > 2 EPS edges
-          uint32_t cl;
-          float v;
-          bool ok;
-          rec_load(base, rend, (int)e0.y, cl, v, ok);
-          pick_update(cl, v, ok);
-        }
-        e0 = e1;
-        e1 = e2;
-        p0 = p1;
-        x0 = x1;
-        r += stride_r;
-      }
-    };
-    if (wave < dense_waves) dense();
-    sparse();
+  // Windows of U sub-steps: window i of wave w is w + i * waves (static interleave), or
+  // (handout, plan->bwd_handout 2) the next one handed out, in stream order, by an LDS counter
+  // (one ds_add_rtn per window per wave), so a wave slowed by CAS retries or misses takes
+  // fewer windows (the LDS-staged dense-run candidate owed its gain to this).
+  const int wave = threadIdx.x / kWave;
+  constexpr int kWaves = NT / kWave;
+  for (int i = 0;; ++i) {
+    int w = wave + i * kWaves;
+    if (handout) {
+      int c = 0;
+      if (lane == 0) c = atomicAdd(&s_next, 1);
+      w = __builtin_amdgcn_readlane(c, 0);
+    }
+    const int base = t.e0 + w * (EPS * U);
+    if (base >= t.e1) break;
+    gather_window(base, t.e1);
   }
   __syncthreads();
 
@@ -1364,7 +1288,7 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
                        lds, s, plan->fwd_tasks, plan->fwd_phase_off, plan->fwd_phases,      \
                        plan->fwd_cv, sp_data, sp_index, recp, rec_bytes, out, D, k,         \
                        plan->fwd_rot_ticks, seltab, is, ds, accum, fix_tab, xstat, xs_n,     \
-                       xs_stride, xs_off2);                                                 \
+                       xs_stride, xs_off2, plan->fwd_handout == 2 ? 1 : 0);                 \
   } while (0)
   if (k % 4 == 0 || plan->fwd_chunk3) {
     switch (FL) {
@@ -1535,35 +1459,25 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   const int F = plan->bwd_feats, ns = plan->bwd_ks;
   const int L = ns / F;
   const uint32_t g_bytes = plan->bwd_big ? 0u : (uint32_t)((uint64_t)N * D * 4u);
-  const bool hy = plan->n_bwd_runs > 0 && !plan->bwd_big;
-  // LDS: accumulators + selectors, then (dense runs) one 1 KB staged row per wave
-  const size_t stage_off = (bwd_lds_bytes(plan->bwd_block_cols, ns) + 15) / 16 * 16;
-  const size_t lds = hy ? stage_off + (size_t)plan->bwd_dense_waves * kBwdStageBytes
-                        : bwd_lds_bytes(plan->bwd_block_cols, ns);
+  const size_t lds = bwd_lds_bytes(plan->bwd_block_cols, ns);
   const dim3 grid(plan->n_bwd_tasks);
   const bool Q = L % 4 == 0;  // quad-aligned lane groups: batched record loads
   const int U = plan->bwd_unroll, W = plan->bwd_waves;
-#define BWD_LAUNCH(UU, NT, FF, QQ, BB, HH)                                                  \
+#define BWD_LAUNCH(UU, NT, FF, QQ, BB)                                                      \
   do {                                                                                      \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, FF, QQ, BB, HH>, lds)); \
-    hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, FF, QQ, BB, HH>), grid, dim3(NT), lds, s, \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(sspmm_bwd4_kernel<UU, NT, FF, QQ, BB>, lds)); \
+    hipLaunchKernelGGL((sspmm_bwd4_kernel<UU, NT, FF, QQ, BB>), grid, dim3(NT), lds, s,     \
                        plan->bwd_tasks, plan->bwd_rec, grad_out, g_bytes, D, sp_index, is,  \
-                       grad_sp, k, ns, slab, plan->bwd_corder, plan->bwd_runs,              \
-                       plan->bwd_dense_waves, (int)stage_off);                              \
-  } while (0)
-#define BWD_SHAPES_H(FF, QQ, HH)                                                            \
-  do {                                                                                      \
-    if (W == 16) BWD_LAUNCH(8, 1024, FF, QQ, false, HH);                                    \
-    else if (W == 12) BWD_LAUNCH(8, 768, FF, QQ, false, HH);                                \
-    else if (U == 16) BWD_LAUNCH(16, 512, FF, QQ, false, HH);                               \
-    else if (U == 12) BWD_LAUNCH(12, 512, FF, QQ, false, HH);                               \
-    else BWD_LAUNCH(8, 512, FF, QQ, false, HH);                                             \
+                       grad_sp, k, ns, slab, plan->bwd_corder, plan->bwd_handout == 2 ? 1 : 0); \
   } while (0)
 #define BWD_SHAPES(FF, QQ)                                                                  \
   do {                                                                                      \
-    if (plan->bwd_big) BWD_LAUNCH(8, 512, FF, QQ, true, false);                             \
-    else if (hy) BWD_SHAPES_H(FF, QQ, true);                                                \
-    else BWD_SHAPES_H(FF, QQ, false);                                                       \
+    if (plan->bwd_big) BWD_LAUNCH(8, 512, FF, QQ, true);                                    \
+    else if (W == 16) BWD_LAUNCH(8, 1024, FF, QQ, false);                                   \
+    else if (W == 12) BWD_LAUNCH(8, 768, FF, QQ, false);                                    \
+    else if (U == 16) BWD_LAUNCH(16, 512, FF, QQ, false);                                   \
+    else if (U == 12) BWD_LAUNCH(12, 512, FF, QQ, false);                                   \
+    else BWD_LAUNCH(8, 512, FF, QQ, false);                                                 \
   } while (0)
   if (F == 4) {
     if (Q) BWD_SHAPES(4, true);
@@ -1572,7 +1486,6 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     if (Q) BWD_SHAPES(2, true);
     else BWD_SHAPES(2, false);
   }
-#undef BWD_SHAPES_H
 #undef BWD_SHAPES
 #undef BWD_LAUNCH
   MAXK_LAUNCH_CHECK("sspmm_bwd launch");

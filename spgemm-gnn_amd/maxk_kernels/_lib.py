@@ -115,8 +115,8 @@ class PlanOptions(ctypes.Structure):
         ("bwd_tp_chunks", _i32),
         ("bwd_row_order", _i32),
         # round 5
-        ("bwd_dense_min", _i32),
-        ("bwd_dense_waves", _i32),
+        ("fwd_handout", _i32),
+        ("bwd_handout", _i32),
     ]
 
 
@@ -151,9 +151,8 @@ class PlanInfo(ctypes.Structure):
         ("bwd_row_order", _i32),
         ("bwd_workspace_peak", _i64),
         # round 5
-        ("bwd_dense_edges", _i64),
-        ("bwd_dense_runs", _i32),
-        ("bwd_dense_min", _i32),
+        ("fwd_handout", _i32),
+        ("bwd_handout", _i32),
     ]
 
     def as_dict(self):
