@@ -39,6 +39,7 @@ from .autograd import (  # noqa: F401
     spgemm,
 )
 
+from . import torch_ops  # noqa: F401,E402  (registers torch.ops.maxk.*)
 from .layers import (  # noqa: F401,E402
     MaxKGCN,
     MaxKGCNConv,
