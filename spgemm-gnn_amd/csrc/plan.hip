@@ -1303,10 +1303,11 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   if (o.bwd_waves == 0 && p->n_bwd_tasks > 0 && p->n_bwd_tasks <= cus) p->bwd_waves = 12;
   // the unroll that actually launches: the 12/16-wave and > 4 GiB shapes run U = 8
   if (p->bwd_waves != 8 || p->bwd_big) p->bwd_unroll = 8;
-  // window hand-out: an LDS counter for the backward when work-groups run in
-  // more than one round, the static interleave otherwise and for the forward
-  p->bwd_handout = o.bwd_handout ? o.bwd_handout : (p->n_bwd_tasks > cus ? 2 : 1);
-  p->fwd_handout = o.fwd_handout ? o.fwd_handout : 1;
+  // window hand-out (profiles/r05/handout_ab.jsonl): the backward always takes
+  // its windows from an LDS counter (k = 8..64 -2..-6 %, W = 8 shards -2 %); the forward at
+  // k <= 16 (-0.3 %, W = 8 shards -1..-5 %), the static interleave above (+2..3 % dynamic)
+  p->bwd_handout = o.bwd_handout ? o.bwd_handout : 2;
+  p->fwd_handout = o.fwd_handout ? o.fwd_handout : (k <= 16 ? 2 : 1);
   if (!btasks.empty()) {
     PLAN_TRY(hipMalloc(&p->bwd_tasks, sizeof(BwdTask) * btasks.size()));
     PLAN_TRY(hipMemcpyAsync(p->bwd_tasks, btasks.data(), sizeof(BwdTask) * btasks.size(),
