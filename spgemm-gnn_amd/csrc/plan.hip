@@ -542,7 +542,8 @@ static int check_options(const maxk_plan_options& o) {
   MAXK_CHECK_ARG(o.bwd_algo >= 0 && o.bwd_algo <= 3,
                  "maxk_plan_create: bwd_algo must be 0 (auto), 1 (column blocks) or 3 (two-pass)");
   MAXK_CHECK_REMOVED(o.bwd_algo != 2, "bwd_algo = 2 (column-major)");
-  MAXK_CHECK_REMOVED(o.fwd_waves == 0 || o.fwd_waves == 4, "fwd_waves other than 4");
+  MAXK_CHECK_ARG(o.fwd_waves == 0 || o.fwd_waves == 4 || o.fwd_waves == 8,
+                 "maxk_plan_create: fwd_waves must be 0, 4 or 8");
   MAXK_CHECK_ARG(o.bwd_waves == 0 || o.bwd_waves == 8 || o.bwd_waves == 12 || o.bwd_waves == 16,
                  "maxk_plan_create: bwd_waves must be 0, 8, 12 or 16");
   MAXK_CHECK_ARG(o.fwd_handout >= 0 && o.fwd_handout <= 2 && o.bwd_handout >= 0 && o.bwd_handout <= 2,
@@ -621,6 +622,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   p->cus = device_cus();
   const int cus = p->cus;
   p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
+  p->fwd_waves = o.fwd_waves ? o.fwd_waves : 4;
   // lane-chunk records by default where the 4-values-per-lane layout fits k badly (Reddit:
   // k = 8 0.95 vs 1.02 ms, k = 24 1.93 vs 2.09 ms; k = 16 / 32 / 64 are slower with chunks),
   // and for every k % 4 != 0 up to 192 (beyond: one lane per feature, f64)
@@ -1297,17 +1299,27 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   }
   p->n_bwd_tasks = (int32_t)btasks.size();
   p->n_bwd_shared = nshared;
-  // One round of tasks (at most one work-group per CU, e.g. an 8-GPU row shard: 256 tasks):
-  // the CU then has only that work-group's waves to hide its gathers, so give it 12 (an
-  // 8-GPU Reddit shard at k = 16: 0.227 -> 0.206 ms; 16 waves profiles/r05/w8_bwd_waves.jsonl)
-  if (o.bwd_waves == 0 && p->n_bwd_tasks > 0 && p->n_bwd_tasks <= cus) p->bwd_waves = 12;
-  // the unroll that actually launches: the 12/16-wave and > 4 GiB shapes run U = 8 (ADVICE r04)
-  if (p->bwd_waves != 8 || p->bwd_big) p->bwd_unroll = 8;
   // window hand-out (profiles/r05/handout_ab.jsonl): the backward always takes
   // its windows from an LDS counter (k = 8..64 -2..-6 %, W = 8 shards -2 %); the forward at
   // k <= 16 (-0.3 %, W = 8 shards -1..-5 %), the static interleave above (+2..3 % dynamic)
   p->bwd_handout = o.bwd_handout ? o.bwd_handout : 2;
   p->fwd_handout = o.fwd_handout ? o.fwd_handout : (k <= 16 ? 2 : 1);
+  if (o.bwd_waves == 0) {
+    if (p->bwd_handout == 2 && !p->bwd_big) {
+      // handed-out windows leave no wave a longer share than its neighbours, so more waves
+      // only add latency hiding: 16 per work-group (Reddit k = 16 1.646 -> 1.504 ms, k = 64
+      // 4.257 -> 4.035, ogbn-proteins k = 16 1.191 -> 0.972; k = 10 / 12 within 0.4 % of
+      // 12 waves; an 8-GPU shard 0.365 -> 0.363; profiles/r05/bwd_waves_handout.jsonl)
+      p->bwd_waves = 16;
+    } else if (p->n_bwd_tasks > 0 && p->n_bwd_tasks <= cus) {
+      // static interleave, one round of tasks (at most one work-group per CU, e.g. an 8-GPU
+      // row shard: 256 tasks): the CU has only that work-group's waves to hide its gathers
+      // (k = 16: 0.227 -> 0.206 ms with 12; profiles/r05/w8_bwd_waves.jsonl)
+      p->bwd_waves = 12;
+    }
+  }
+  // the unroll that actually launches: the 12/16-wave and > 4 GiB shapes run U = 8 (ADVICE r04)
+  if (p->bwd_waves != 8 || p->bwd_big) p->bwd_unroll = 8;
   if (!btasks.empty()) {
     PLAN_TRY(hipMalloc(&p->bwd_tasks, sizeof(BwdTask) * btasks.size()));
     PLAN_TRY(hipMemcpyAsync(p->bwd_tasks, btasks.data(), sizeof(BwdTask) * btasks.size(),

@@ -426,8 +426,8 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
 // reuse). accum: the rows of out hold a prior sum to add to (the multi-GPU split's remote
 // part). VEC == 1: k % 4 != 0 beyond the lane chunks' range (k > 192), min(k, 64) lanes per
 // edge looping over the row's k entries, f64 atomics.
-template <int VEC, int FL>
-__global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
+template <int VEC, int FL, int NT>
+__global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     const FwdTask* __restrict__ tasks, const int32_t* __restrict__ phase_off, int phases,
     const uint2* __restrict__ cv, const float* __restrict__ sp_data,
     const uint8_t* __restrict__ sp_index, const uint8_t* __restrict__ rec, int rec_bytes,
@@ -470,12 +470,12 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   const int DS = D + kFwdRowPad;  // LDS row stride (elements)
   if (accum && !split && !fixed) {  // continue from the stored rows
     const float* src = out + (size_t)t.row0 * D;
-    for (int i = threadIdx.x; i < n; i += kFwdThreads) {
+    for (int i = threadIdx.x; i < n; i += NT) {
       const int r = i / D;
       acc[r * DS + (i - r * D)] = src[i];
     }
   } else {
-    for (int i = threadIdx.x; i < nrows * DS; i += kFwdThreads) acc[i] = 0.0;
+    for (int i = threadIdx.x; i < nrows * DS; i += NT) acc[i] = 0.0;
   }
   __syncthreads();
 
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   const int slot = lane / L;
   const int l0 = (lane - slot * L) * (C3 ? 1 : VEC);
   const bool lane_on = slot < EPS;
-  constexpr int kWaves = kFwdThreads / kWave;
+  constexpr int kWaves = NT / kWave;
 
   if constexpr (VEC == 4) {
     auto sweep = [&](auto* a, auto tag) {
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
   if (!split) {
     const bool add = accum && fixed;  // the prior row is added here (see above)
     if ((D & 3) == 0) {
-      for (int i = threadIdx.x * 4; i < n; i += kFwdThreads * 4) {
+      for (int i = threadIdx.x * 4; i < n; i += NT * 4) {
         float4 v = make_float4(get(i), get(i + 1), get(i + 2), get(i + 3));
         if (add) {
           const float4 o = *reinterpret_cast<const float4*>(dst + i);
@@ -540,10 +540,10 @@ __global__ __launch_bounds__(kFwdThreads) void spgemm_fwd_kernel(
         *reinterpret_cast<float4*>(dst + i) = v;
       }
     } else {
-      for (int i = threadIdx.x; i < n; i += kFwdThreads) dst[i] = add ? dst[i] + get(i) : get(i);
+      for (int i = threadIdx.x; i < n; i += NT) dst[i] = add ? dst[i] + get(i) : get(i);
     }
   } else {
-    for (int i = threadIdx.x; i < D; i += kFwdThreads) global_add(dst + i, get(i));
+    for (int i = threadIdx.x; i < D; i += NT) global_add(dst + i, get(i));
   }
 }
 
@@ -1281,14 +1281,19 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   const int Lf = plan->fwd_chunk3 ? (k + 2) / 3 : k / 4;  // lanes per edge
   const int FL = (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0) |
                  (plan->fwd_quad && Lf % 4 == 0 ? kFwdFlagQuad : 0);
-#define FWD_LAUNCH(V, FF)                                                                   \
+#define FWD_LAUNCH_NT(V, FF, NT)                                                            \
   do {                                                                                      \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, FF>, lds));             \
-    hipLaunchKernelGGL((spgemm_fwd_kernel<V, FF>), dim3(plan->n_fwd_tasks), dim3(kFwdThreads), \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, FF, NT>, lds));         \
+    hipLaunchKernelGGL((spgemm_fwd_kernel<V, FF, NT>), dim3(plan->n_fwd_tasks), dim3(NT),    \
                        lds, s, plan->fwd_tasks, plan->fwd_phase_off, plan->fwd_phases,      \
                        plan->fwd_cv, sp_data, sp_index, recp, rec_bytes, out, D, k,         \
                        plan->fwd_rot_ticks, seltab, is, ds, accum, fix_tab, xstat, xs_n,     \
                        xs_stride, xs_off2, plan->fwd_handout == 2 ? 1 : 0);                 \
+  } while (0)
+#define FWD_LAUNCH(V, FF)                                                                   \
+  do {                                                                                      \
+    if (plan->fwd_waves == 8) FWD_LAUNCH_NT(V, FF, 8 * kWave);                              \
+    else FWD_LAUNCH_NT(V, FF, kFwdThreads);                                                 \
   } while (0)
   if (k % 4 == 0 || plan->fwd_chunk3) {
     switch (FL) {
@@ -1301,6 +1306,7 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     FWD_LAUNCH(1, 0);
   }
 #undef FWD_LAUNCH
+#undef FWD_LAUNCH_NT
   MAXK_LAUNCH_CHECK("spgemm_fwd launch");
   return MAXK_OK;
 }

@@ -609,6 +609,9 @@ PLAN_OPTIONS = [
     dict(bwd_handout=1), dict(bwd_handout=2), dict(bwd_handout=2, bwd_piece_edges=500, bwd_waves=12),
     dict(bwd_handout=2, bwd_features_per_lane=2), dict(fwd_handout=2), dict(fwd_handout=2, fwd_rotate=2),
     dict(fwd_handout=2, fwd_tile_rows=1),
+    # 8 waves per forward work-group, static and counter hand-out, one-row tiles
+    dict(fwd_waves=8), dict(fwd_waves=8, fwd_handout=1), dict(fwd_waves=8, fwd_tile_rows=1),
+    dict(fwd_waves=8, fwd_chunk3=1), dict(fwd_waves=8, fwd_fixed=2),
     dict(bwd_slot_groups=2), dict(bwd_slot_groups=4), dict(bwd_lds_bytes=4096),
     dict(bwd_tasks_per_cu=1), dict(bwd_algo=3), dict(bwd_algo="two_pass"),
     # the accepted spellings of the defaults of removed knobs
@@ -663,7 +666,7 @@ PLAN_OPTIONS = [
 REMOVED_OPTIONS = [
     dict(fwd_accumulator="f32_cas"), dict(bwd_accumulator="f64"), dict(bwd_features_per_lane=1),
     dict(fwd_phases=3), dict(fwd_persistent=1), dict(fwd_unroll=16), dict(bwd_order=1),
-    dict(bwd_acc_pad=1), dict(bwd_sel_lds=2), dict(bwd_algo=2), dict(fwd_waves=8),
+    dict(bwd_acc_pad=1), dict(bwd_sel_lds=2), dict(bwd_algo=2),
     dict(fwd_prefetch=1), dict(bwd_prefetch=1), dict(fwd_record_bytes=256), dict(fwd_branchless=2),
     dict(bwd_cas64=2), dict(quad_loads=1), dict(quad_loads=2), dict(bwd_chunk_bounds=1),
     dict(bwd_chunk_bounds=3), dict(bwd_tp_store=2), dict(bwd_row_cost=8), dict(col_order=3),
@@ -671,7 +674,7 @@ REMOVED_OPTIONS = [
 INVALID_OPTIONS = [
     dict(bwd_unroll=7), dict(bwd_unroll=4), dict(bwd_slot_groups=3), dict(fwd_tile_rows=65),
     dict(bwd_lds_bytes=1 << 20), dict(bwd_algo=4), dict(bwd_waves=20), dict(fwd_chunk3=3),
-    dict(bwd_handout=3), dict(fwd_handout=-1),
+    dict(bwd_handout=3), dict(fwd_handout=-1), dict(fwd_waves=6), dict(fwd_waves=16),
     dict(fwd_two_tables=3), dict(bwd_flush=3), dict(bwd_piece_edges=-1), dict(bwd_chunk_bounds=4),
     dict(col_order=5), dict(col_order=4), dict(bwd_tp_chunks=-2), dict(bwd_row_order=3),
     dict(bwd_features_per_lane=3), dict(fwd_fixed=3), dict(external_workspace=2), dict(bwd_order=4), dict(fwd_rotate=3),
