@@ -160,6 +160,7 @@ struct maxk_plan {
   // ---- forward: tiles of whole rows (FwdTask), edges column-sorted per tile
   int32_t fwd_tile_rows = 32;
   int32_t fwd_waves = 4;        // wavefronts per forward work-group (4 or 8)
+  int32_t fwd_unroll = 8;       // forward sub-steps in flight per wave (4 only with 8 waves)
   int32_t fwd_rec_bytes = 0;     // packed CBSR record size (per-call pack)
   uint8_t* fwd_rec = nullptr;    // [num_cols][fwd_rec_bytes] plan-owned workspace
   // fixed-point forward (LdsFix): per task {sexp, gexp} (fwd_fix_stats_kernel); the call's

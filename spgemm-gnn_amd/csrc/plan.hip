@@ -526,7 +526,10 @@ static int check_options(const maxk_plan_options& o) {
   MAXK_CHECK_REMOVED(o.bwd_features_per_lane != 1, "bwd_features_per_lane = 1");
   MAXK_CHECK_REMOVED(o.fwd_phases <= 1, "fwd_phases > 1");
   MAXK_CHECK_REMOVED(o.fwd_persistent == 0, "fwd_persistent");
-  MAXK_CHECK_REMOVED(o.fwd_unroll == 0 || o.fwd_unroll == 8, "fwd_unroll other than 8");
+  MAXK_CHECK_REMOVED(o.fwd_unroll == 0 || o.fwd_unroll == 8 || o.fwd_unroll == 4,
+                     "fwd_unroll other than 4 or 8");
+  MAXK_CHECK_ARG(o.fwd_unroll != 4 || o.fwd_waves != 4,
+                 "maxk_plan_create: fwd_unroll 4 needs 8 forward waves");
   MAXK_CHECK_ARG(o.bwd_unroll == 0 || o.bwd_unroll == 8 || o.bwd_unroll == 12 ||
                      o.bwd_unroll == 16,
                  "maxk_plan_create: bwd_unroll must be 0, 8, 12 or 16");
@@ -622,7 +625,13 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   p->cus = device_cus();
   const int cus = p->cus;
   p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows : kFwdTileRows;
-  p->fwd_waves = o.fwd_waves ? o.fwd_waves : 4;
+  // 8 waves per forward work-group, their windows from an LDS counter (below): more gathers
+  // in flight per CU (Reddit k = 8 / 32 / 64 -4 / -7 / -9 %, k = 20..60 -4..-24 %), except
+  // where the 4-wave sweep's column span is what keeps the records in L2: k = 16 (8 waves
+  // +36 %, L2 hit 62 -> 37 %) and k = 48 (+28 %; 4 sub-steps per wave instead, -4 %).
+  // profiles/r05/fwd_waves_sweep.jsonl
+  p->fwd_waves = o.fwd_waves ? o.fwd_waves : (k == 16 && o.fwd_unroll != 4 ? 4 : 8);
+  p->fwd_unroll = o.fwd_unroll ? o.fwd_unroll : (p->fwd_waves == 8 && k == 48 ? 4 : 8);
   // lane-chunk records by default where the 4-values-per-lane layout fits k badly (Reddit:
   // k = 8 0.95 vs 1.02 ms, k = 24 1.93 vs 2.09 ms; k = 16 / 32 / 64 are slower with chunks),
   // and for every k % 4 != 0 up to 192 (beyond: one lane per feature, f64)
@@ -1300,10 +1309,11 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   p->n_bwd_tasks = (int32_t)btasks.size();
   p->n_bwd_shared = nshared;
   // window hand-out (profiles/r05/handout_ab.jsonl): the backward always takes
-  // its windows from an LDS counter (k = 8..64 -2..-6 %, W = 8 shards -2 %); the forward at
-  // k <= 16 (-0.3 %, W = 8 shards -1..-5 %), the static interleave above (+2..3 % dynamic)
+  // its windows from an LDS counter (k = 8..64 -2..-6 %, W = 8 shards -2 %); the forward with
+  // 8 waves and at k <= 16 (-0.3 %, W = 8 shards -1..-5 %); 4 waves above k = 16 keep the
+  // static interleave (+2..3 % with the counter)
   p->bwd_handout = o.bwd_handout ? o.bwd_handout : 2;
-  p->fwd_handout = o.fwd_handout ? o.fwd_handout : (k <= 16 ? 2 : 1);
+  p->fwd_handout = o.fwd_handout ? o.fwd_handout : (k <= 16 || p->fwd_waves == 8 ? 2 : 1);
   if (o.bwd_waves == 0) {
     if (p->bwd_handout == 2 && !p->bwd_big) {
       // handed-out windows leave no wave a longer share than its neighbours, so more waves
@@ -1413,6 +1423,10 @@ extern "C" int maxk_plan_get_info_sized(const maxk_plan* p, maxk_plan_info* out,
   info.bwd_workspace_peak = p->bwd_ws_bytes;
   info.fwd_handout = p->fwd_handout;
   info.bwd_handout = p->bwd_handout;
+  info.fwd_waves = p->fwd_waves;
+  info.fwd_unroll = p->fwd_unroll;
+  info.bwd_waves = p->bwd_waves;
+  info.bwd_unroll = p->bwd_unroll;
   std::memcpy(out, &info, (size_t)std::min<int64_t>(info_bytes, (int64_t)sizeof(maxk_plan_info)));
   return MAXK_OK;
 }

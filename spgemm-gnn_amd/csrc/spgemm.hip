@@ -317,7 +317,7 @@ __global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
 }
 
 // One wave's share of the forward edges [e0, e1) (4 features per lane, or lane chunks):
-// U = kFwdUnroll sub-steps per iteration with every load issued before the first LDS update.
+// U sub-steps per iteration (kFwdUnroll; 4 with 8 waves by option) with every load issued before the first LDS update.
 // The chain (col, val) -> CBSR record -> LDS has two dependent global round trips, so
 // memory-level parallelism comes from U independent sub-steps per wave. Idle lanes load a
 // clamped (valid) edge and add 0 at its addresses instead of branching (with a branch the
@@ -328,7 +328,7 @@ __global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
 // DPP hands it to the quad: one edge-word instruction per four sub-steps.
 // (Batching the selector words the same way, 64 scattered records per instruction, ran k = 16
 // 1.10 -> 1.48 ms: only contiguous loads gain from fewer instructions.)
-template <class A, int FL>
+template <class A, int FL, int U>
 __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, int* ctr,
                                            int wave, int nwaves, int EPS, int slot, int l0,
                                            bool lane_on,
@@ -337,7 +337,6 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
                                            const uint8_t* __restrict__ seltab, int ss, int D,
                                            int k, double sc) {
   using T = typename A::T;
-  constexpr int U = kFwdUnroll;
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
   constexpr bool EM = (FL & kFwdFlagQuad) != 0;
   const int last = e1 - 1;
@@ -426,7 +425,7 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
 // reuse). accum: the rows of out hold a prior sum to add to (the multi-GPU split's remote
 // part). VEC == 1: k % 4 != 0 beyond the lane chunks' range (k > 192), min(k, 64) lanes per
 // edge looping over the row's k entries, f64 atomics.
-template <int VEC, int FL, int NT>
+template <int VEC, int FL, int NT, int FU>
 __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
     const FwdTask* __restrict__ tasks, const int32_t* __restrict__ phase_off, int phases,
     const uint2* __restrict__ cv, const float* __restrict__ sp_data,
@@ -495,12 +494,12 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
       int* c0 = handout ? &s_win[0] : nullptr;
       int* c1 = handout ? &s_win[1] : nullptr;
       if (emid >= 0) {
-        fwd_edges4<AA, FL>(a, emid, t.e1, c0, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+        fwd_edges4<AA, FL, FU>(a, emid, t.e1, c0, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, seltab, ss, DS, k, fsc);
-        fwd_edges4<AA, FL>(a, t.e0, emid, c1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+        fwd_edges4<AA, FL, FU>(a, t.e0, emid, c1, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, seltab, ss, DS, k, fsc);
       } else {
-        fwd_edges4<AA, FL>(a, t.e0, t.e1, c0, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
+        fwd_edges4<AA, FL, FU>(a, t.e0, t.e1, c0, wave, kWaves, EPS, slot, l0, lane_on, cv, rec,
                            rec_bytes, seltab, ss, DS, k, fsc);
       }
     };
@@ -1281,10 +1280,10 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   const int Lf = plan->fwd_chunk3 ? (k + 2) / 3 : k / 4;  // lanes per edge
   const int FL = (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0) |
                  (plan->fwd_quad && Lf % 4 == 0 ? kFwdFlagQuad : 0);
-#define FWD_LAUNCH_NT(V, FF, NT)                                                            \
+#define FWD_LAUNCH_NT(V, FF, NT, FU)                                                        \
   do {                                                                                      \
-    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, FF, NT>, lds));         \
-    hipLaunchKernelGGL((spgemm_fwd_kernel<V, FF, NT>), dim3(plan->n_fwd_tasks), dim3(NT),    \
+    if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, FF, NT, FU>, lds));     \
+    hipLaunchKernelGGL((spgemm_fwd_kernel<V, FF, NT, FU>), dim3(plan->n_fwd_tasks), dim3(NT), \
                        lds, s, plan->fwd_tasks, plan->fwd_phase_off, plan->fwd_phases,      \
                        plan->fwd_cv, sp_data, sp_index, recp, rec_bytes, out, D, k,         \
                        plan->fwd_rot_ticks, seltab, is, ds, accum, fix_tab, xstat, xs_n,     \
@@ -1292,8 +1291,9 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   } while (0)
 #define FWD_LAUNCH(V, FF)                                                                   \
   do {                                                                                      \
-    if (plan->fwd_waves == 8) FWD_LAUNCH_NT(V, FF, 8 * kWave);                              \
-    else FWD_LAUNCH_NT(V, FF, kFwdThreads);                                                 \
+    if (plan->fwd_waves == 8 && plan->fwd_unroll == 4) FWD_LAUNCH_NT(V, FF, 8 * kWave, 4);   \
+    else if (plan->fwd_waves == 8) FWD_LAUNCH_NT(V, FF, 8 * kWave, kFwdUnroll);             \
+    else FWD_LAUNCH_NT(V, FF, kFwdThreads, kFwdUnroll);                                     \
   } while (0)
   if (k % 4 == 0 || plan->fwd_chunk3) {
     switch (FL) {

@@ -153,6 +153,10 @@ class PlanInfo(ctypes.Structure):
         # round 5
         ("fwd_handout", _i32),
         ("bwd_handout", _i32),
+        ("fwd_waves", _i32),
+        ("fwd_unroll", _i32),
+        ("bwd_waves", _i32),
+        ("bwd_unroll", _i32),
     ]
 
     def as_dict(self):

@@ -611,7 +611,9 @@ PLAN_OPTIONS = [
     dict(fwd_handout=2, fwd_tile_rows=1),
     # 8 waves per forward work-group, static and counter hand-out, one-row tiles
     dict(fwd_waves=8), dict(fwd_waves=8, fwd_handout=1), dict(fwd_waves=8, fwd_tile_rows=1),
-    dict(fwd_waves=8, fwd_chunk3=1), dict(fwd_waves=8, fwd_fixed=2),
+    dict(fwd_waves=8, fwd_chunk3=1), dict(fwd_waves=8, fwd_fixed=2), dict(fwd_waves=4),
+    dict(fwd_unroll=4), dict(fwd_waves=8, fwd_unroll=4, fwd_handout=1),
+    dict(fwd_waves=8, fwd_unroll=4, fwd_chunk3=1),
     dict(bwd_slot_groups=2), dict(bwd_slot_groups=4), dict(bwd_lds_bytes=4096),
     dict(bwd_tasks_per_cu=1), dict(bwd_algo=3), dict(bwd_algo="two_pass"),
     # the accepted spellings of the defaults of removed knobs
@@ -675,10 +677,26 @@ INVALID_OPTIONS = [
     dict(bwd_unroll=7), dict(bwd_unroll=4), dict(bwd_slot_groups=3), dict(fwd_tile_rows=65),
     dict(bwd_lds_bytes=1 << 20), dict(bwd_algo=4), dict(bwd_waves=20), dict(fwd_chunk3=3),
     dict(bwd_handout=3), dict(fwd_handout=-1), dict(fwd_waves=6), dict(fwd_waves=16),
+    dict(fwd_waves=4, fwd_unroll=4),
     dict(fwd_two_tables=3), dict(bwd_flush=3), dict(bwd_piece_edges=-1), dict(bwd_chunk_bounds=4),
     dict(col_order=5), dict(col_order=4), dict(bwd_tp_chunks=-2), dict(bwd_row_order=3),
     dict(bwd_features_per_lane=3), dict(fwd_fixed=3), dict(external_workspace=2), dict(bwd_order=4), dict(fwd_rotate=3),
 ]
+
+
+@pytest.mark.parametrize("k,fw,fu,fh", [(8, 8, 8, 2), (16, 4, 8, 2), (32, 8, 8, 2), (48, 8, 4, 2),
+                                         (64, 8, 8, 2)])
+def test_plan_info_reports_launch_shapes(gpu, k, fw, fu, fh):
+    """Round-5 defaults: 8 forward waves with the counter hand-out except
+    4 at k = 16, 4 sub-steps at k = 48; 16 backward waves with the counter."""
+    p, ix, v = GRAPHS["heavy_split"]()
+    n = p.size - 1
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    info = mk.GraphPlan(ptr, idx, val, n, ix.size, 256, k).info()
+    assert (info["fwd_waves"], info["fwd_unroll"], info["fwd_handout"]) == (fw, fu, fh)
+    assert (info["bwd_waves"], info["bwd_unroll"], info["bwd_handout"]) == (16, 8, 2)
+    st = mk.GraphPlan(ptr, idx, val, n, ix.size, 256, k, options={"bwd_handout": 1}).info()
+    assert st["bwd_waves"] in (8, 12) and st["bwd_handout"] == 1
 
 
 @pytest.mark.parametrize("opts", PLAN_OPTIONS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
