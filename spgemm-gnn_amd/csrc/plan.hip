@@ -1161,18 +1161,28 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     nch64 = std::max<int64_t>(1, nch64);
     // One work-group per CU: a task count just past a multiple of the CUs leaves the last
     // round mostly idle (ogbn-proteins k = 32: 192 blocks x 3 chunks = 2.25 rounds, 2.37 ms;
-    // x 4 = 3 rounds, 1.82 ms). With the default knobs take the chunk count in [nch, nch + 2]
-    // whose tasks fill their rounds best, keeping >= 0.6 x the minimum task.
+    // x 4 = 3 rounds, 1.82 ms). With the default knobs take, among the chunk counts from one
+    // round of tasks (fl) up to nch + 2 (keeping >= 0.6 x the minimum task above nch), the
+    // FEWEST whose tasks fill their rounds within 0.05 of the best: every task zeroes and
+    // stores its block and stages its selectors, so with the counter-fed 16-wave work-groups
+    // one full round beats two (Reddit k = 8 / 16 / 32: 512 -> 256 tasks -2.8 / -2.0 / -1.8 %,
+    // ogbn-proteins k = 16 -1.4 %; profiles/r05/bwd_task_rounds.jsonl)
     if (o.bwd_tasks_per_cu == 0 && o.bwd_min_task_edges == 0) {
       auto fill = [&](int64_t c) {
         const int64_t t = bS * c;
         return (double)t / ((double)((t + cus - 1) / cus) * cus);
       };
-      int64_t best = nch64;
+      const int64_t lo = std::max<int64_t>(1, std::min(nch64, fl));
+      int64_t hi = nch64;
       for (int64_t c = nch64 + 1; c <= nch64 + 2; ++c) {
         if ((double)E / ((double)nblocks * c) < 0.6 * kBwdMinTaskEdges) break;
-        if (fill(c) > fill(best) + 0.05) best = c;
+        hi = c;
       }
+      double bestf = 0.0;
+      for (int64_t c = lo; c <= hi; ++c) bestf = std::max(bestf, fill(c));
+      int64_t best = hi;
+      for (int64_t c = lo; c <= hi; ++c)
+        if (fill(c) >= bestf - 0.05) { best = c; break; }
       nch64 = best;
     }
     const int nch = (int)nch64;
