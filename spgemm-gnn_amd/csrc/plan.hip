@@ -1338,8 +1338,10 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       p->bwd_waves = 12;
     }
   }
-  // the unroll that actually launches: the 12/16-wave and > 4 GiB shapes run U = 8
-  if (p->bwd_waves != 8 || p->bwd_big) p->bwd_unroll = 8;
+  // the unroll that actually launches: the 16-wave and > 4 GiB shapes run U = 8, 12 waves U =
+  // 8 or 12
+  if ((p->bwd_waves != 8 && !(p->bwd_waves == 12 && p->bwd_unroll == 12)) || p->bwd_big)
+    p->bwd_unroll = 8;
   if (!btasks.empty()) {
     PLAN_TRY(hipMalloc(&p->bwd_tasks, sizeof(BwdTask) * btasks.size()));
     PLAN_TRY(hipMemcpyAsync(p->bwd_tasks, btasks.data(), sizeof(BwdTask) * btasks.size(),

@@ -1480,6 +1480,7 @@ static int sspmm_backward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   do {                                                                                      \
     if (plan->bwd_big) BWD_LAUNCH(8, 512, FF, QQ, true);                                    \
     else if (W == 16) BWD_LAUNCH(8, 1024, FF, QQ, false);                                   \
+    else if (W == 12 && U == 12) BWD_LAUNCH(12, 768, FF, QQ, false);                       \
     else if (W == 12) BWD_LAUNCH(8, 768, FF, QQ, false);                                    \
     else if (U == 16) BWD_LAUNCH(16, 512, FF, QQ, false);                                   \
     else if (U == 12) BWD_LAUNCH(12, 512, FF, QQ, false);                                   \
