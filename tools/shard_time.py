@@ -9,6 +9,7 @@ collectives), to see how the compute part strong-scales:
             packed per call or gathered as two tables)
 
   python tools/shard_time.py [--k 16] [--worlds 1,2,4,8] [--opts '{}'] [--layouts records,tables]
+                            [--all-ranks]
 """
 import argparse
 import json
@@ -46,6 +47,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--opts", default="{}", help="plan options (JSON dict)")
     ap.add_argument("--layouts", default="records,tables")
+    ap.add_argument("--all-ranks", action="store_true", help="time every rank, not 0 and W-1")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS[args.dataset]
@@ -60,7 +62,7 @@ def main():
         part = RowPartition(ptr, world)
         for layout in args.layouts.split(","):
             worst = 0.0
-            for q in sorted({0, world - 1}):
+            for q in (range(world) if args.all_ranks else sorted({0, world - 1})):
                 a, b = part.rows(q)
                 idx_q = graphs.synthetic_rows(ptr, seed=97, rows=(a, b))
                 val_q = graphs.sage_mean_values(ptr[a:b + 1], num_edges=idx_q.numel())
