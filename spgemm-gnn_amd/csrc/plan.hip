@@ -850,7 +850,11 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     // turn), so the tiles running together on an XCD gather from nearby columns (L2 reuse).
     int B = 1;
     p->fwd_rot_ticks = 0;
-    if (o.fwd_rotate != 2 && (k % 4 == 0 || p->fwd_chunk3)) {
+    // Not on graphs whose columns see few edges: each record is then used ~E / NC times over
+    // the whole pass and the aligned sweep finds little to share (ogbn-products, 50 edges per
+    // column, k = 32: 4.79 -> 4.71 ms without it; Reddit, 493: k = 16 1.11 -> 1.08 with it)
+    const bool low_reuse = o.fwd_rotate == 0 && NC > 0 && (double)E / NC < 64.0;
+    if (o.fwd_rotate != 2 && !low_reuse && (k % 4 == 0 || p->fwd_chunk3)) {
       // the fixed-point kernel sweeps faster: more windows at large k, a higher slot rate
       // (tools/fwd_opts_sweep.py, Reddit: k = 16 1.23 -> 1.19 ms with 260 M edges/s per slot,
       // k = 32 1.81 -> 1.77 with 140 M and 32 windows, k = 64 3.44 -> 3.23 with 64 windows)
