@@ -10,15 +10,16 @@
 // integer LDS atomic rate (tools/ubench_atomics.hip, profiles/r01/ubench_atomics.log), so
 // both kernels are restructured:
 //
-//   forward : a 256-thread work-group owns <= 32 whole destination rows (LDS accumulator
-//             rows x D); its edges are processed flat, k/4 lanes per edge, 4 features per
+//   forward : a 256- or 512-thread work-group (4 or 8 waves) owns <= 32 whole destination
+//             rows (LDS accumulator rows x D); its waves take edge windows from an LDS counter
+//             (or a static interleave); the edges are processed flat, k/4 lanes per edge, 4 features per
 //             lane (one dwordx4 value gather + one dword selector gather; or lane chunks of
 //             3 values + their selectors for k % 16 != 0), 8 independent sub-steps in
-//             flight per wave; products are accumulated in LDS in exact fixed point
+//             flight per wave (4 at k = 48); products are accumulated in LDS in exact fixed point
 //             (ds_add_u64, LdsFix) or f64 (ds_add_f64), and the rows are written back once
 //             with coalesced dwordx4 stores. Only rows longer than the task cap are split,
 //             and only those touch global atomics.
-//   backward: a 512/768-thread work-group owns a block of source columns whose k-wide
+//   backward: a 512/768/1024-thread work-group owns a block of source columns whose k-wide
 //             gradients live in LDS; it sweeps the block's edges in destination-row order
 //             (plan-built block-major edge list), so the lanes of one instruction gather
 //             from few rows of grad_out (L1 reuse); updates are 64-bit compare-and-swaps on
