@@ -64,6 +64,22 @@ def test_graph_shape(case):
     assert ptr.numel() == n + 1 and idx.numel() == e and int(ptr[-1]) == e
 
 
+def test_backward_tasks_fill_their_rounds(case):
+    """Round-5 task count (plan.hip): one work-group per CU runs the column-block
+    tasks in rounds, and the plan picks the chunk count whose rounds are filled best (the
+    fewest chunks within 0.05): no config's last round is mostly idle."""
+    ptr, idx, val, _, _, _, name, K, _ = case
+    N, E = ptr.numel() - 1, idx.numel()
+    info = mk.GraphPlan(ptr, idx, val, N, E, D, K).info()
+    if info["bwd_algo"] != 1:
+        pytest.skip("two-pass backward: no column-block tasks")
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    t = info["bwd_tasks"]
+    rounds = -(-t // cus)
+    print(f"{name} k={K}: {t} tasks, {rounds} rounds, fill {t / (rounds * cus):.2f}")
+    assert t / (rounds * cus) >= 0.85
+
+
 def test_adjoint_and_linearity(case):
     ptr, idx, val, sp_data, sp_index, g, _, K, _ = case
     N, E = ptr.numel() - 1, idx.numel()
