@@ -641,6 +641,13 @@ __device__ __forceinline__ void bwd_cas_update(unsigned* accq, int KS, const uin
   }
 }
 
+// Probe hooks (tools/probe_bwd_tail.hip includes this file with them defined: per-work-group
+// start / end clocks); empty in the library.
+#ifndef MAXK_BWD_PROBE_BEGIN
+#define MAXK_BWD_PROBE_BEGIN()
+#define MAXK_BWD_PROBE_END()
+#endif
+
 template <int U, int NT, int F, bool Q, bool BIG>
 __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     const BwdTask* __restrict__ tasks, const uint32_t* __restrict__ rec,
@@ -654,6 +661,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
   __shared__ int s_next;  // next window of the task's edge stream to hand out
   float* bacc = reinterpret_cast<float*>(bsmem);
   const BwdTask t = tasks[blockIdx.x];
+  MAXK_BWD_PROBE_BEGIN();
   // padding / nothing to add (with the slab flush every piece stores its block, zeros too)
   if (t.ncols == 0 || (t.shared && !slab && t.e0 == t.e1)) return;
   const int L = ns / F;   // lanes per edge
@@ -789,6 +797,7 @@ __global__ __launch_bounds__(NT) void sspmm_bwd4_kernel(
     if (atomic) global_add(dst + row * k + g0 + l, a);
     else dst[row * k + g0 + l] = a;
   }
+  MAXK_BWD_PROBE_END();
 }
 
 // Slab flush, second step: the blocks with several pieces add their slab regions (piece 1, 2,
