@@ -48,6 +48,9 @@ def report(name, plan, fn, reps=5):
                      "p90_us": float(np.percentile(d, 90)), "max_us": float(d.max()),
                      "min_us": float(d.min()),
                      "idle_share": float(1 - d.sum() / (span * conc))})
+    if os.environ.get("PROBE_DUMP"):   # raw clocks of the last launch, with the plan's tasks
+        np.savez(os.path.join(os.environ["PROBE_DUMP"], name.replace(" ", "_").replace("=", "") + ".npz"),
+                 start=s, end=e)
     best = min(rows, key=lambda r: r["span_us"])
     worst = max(rows, key=lambda r: r["span_us"])
     print(json.dumps({"case": name, "tasks": n, "best": best, "worst": worst}), flush=True)
