@@ -340,7 +340,6 @@ __global__ void iota_kernel(int n, int32_t* __restrict__ out) {
   if (i < n) out[i] = i;
 }
 
-
 static void dfree(void* q) { if (q) (void)hipFree(q); }
 
 static int grid_for(int64_t n, int threads) {
@@ -1441,8 +1440,8 @@ extern "C" int maxk_plan_get_info_sized(const maxk_plan* p, maxk_plan_info* out,
   info.bwd_handout = p->bwd_handout;
   info.fwd_waves = p->fwd_waves;
   info.fwd_unroll = p->fwd_unroll;
-  info.bwd_waves = p->bwd_waves;
-  info.bwd_unroll = p->bwd_unroll;
+  info.bwd_waves = p->bwd_twopass ? 0 : p->bwd_waves;  // the two-pass kernels have one shape
+  info.bwd_unroll = p->bwd_twopass ? 0 : p->bwd_unroll;
   std::memcpy(out, &info, (size_t)std::min<int64_t>(info_bytes, (int64_t)sizeof(maxk_plan_info)));
   return MAXK_OK;
 }
