@@ -674,10 +674,14 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   // ~1.9: 3.32 -> 3.25); with more reuse one group stays faster (ogbn-proteins k = 32, ~3.1:
   // 1.82 vs 1.86).
   const int kF = (k + F - 1) / F * F;  // k padded to whole lanes
+  // Round 5 (16 counter-fed waves, one round of tasks): two groups from k = 16 and below 4.5
+  // edges per (block, row) (Reddit, 3.9 at k = 16: 1.468 -> 1.436 ms; k = 24, 2.6: 2.373 ->
+  // 2.110; ogbn-proteins k = 16 / 24 at 8.2 / 5.5 stay at one group, +8 % with two;
+  // profiles/r05/bwd_slot_groups_sweep.jsonl)
   int S = o.bwd_slot_groups ? o.bwd_slot_groups : 1;
-  if (o.bwd_slot_groups == 0 && F == 4 && k >= 32 && k % 8 == 0 && N > 0 && NC > 0) {
+  if (o.bwd_slot_groups == 0 && F == 4 && k >= 16 && k % 8 == 0 && N > 0 && NC > 0) {
     const double c1 = std::min<double>(NC, (lds_budget - 16) / (5.0 * k));
-    if ((double)E / N * c1 / NC < 2.5) S = 2;
+    if ((double)E / N * c1 / NC < 4.5) S = 2;
   }
   while (S > 1 && kF % (F * S) != 0) S >>= 1;
   p->bwd_slot_groups = S;
