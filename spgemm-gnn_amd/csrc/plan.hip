@@ -1304,10 +1304,11 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       p->device_bytes += sizeof(int4) * comb.size();
     }
   }
-  // default on with one slot group (Reddit k = 16: 1.665 -> 1.626 ms, an 8-GPU row shard
-  // 0.241 -> 0.226); with two groups a block's two tasks already share their rows and the
-  // windows measured +0.7-1.5 % (k = 32 / 64, profiles/r04/bwd_order_ab.jsonl)
-  const bool windows = o.bwd_order == 2 || (o.bwd_order == 0 && p->bwd_slot_groups == 1);
+  // default on (Reddit k = 16: 1.665 -> 1.626 ms, an 8-GPU row shard 0.241 -> 0.226). Round 4
+  // measured them +0.7-1.5 % with two slot groups (profiles/r04/bwd_order_ab.jsonl); with the
+  // round-5 kernel (counter-fed 16 waves, one round) they gain there too: k = 16 / 24 / 32 / 64
+  // -1.5 / -0.7 / -0.4 / -0.3 % (profiles/r05/bwd_order_ab.jsonl)
+  const bool windows = o.bwd_order == 2 || o.bwd_order == 0;
   if (windows && btasks.size() >= 2 * (size_t)kXcds) {
     // XCD row windows: work-group i runs on XCD i % 8, one task per CU at a time. Within each
     // round of `cus` consecutive (row-sorted) tasks, XCD x gets the x-th contiguous run of
