@@ -684,6 +684,14 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     if ((double)E / N * c1 / NC < 4.5) S = 2;
   }
   while (S > 1 && kF % (F * S) != 0) S >>= 1;
+  // Two groups of 8 slots (k = 16): two slots per lane, so an edge keeps 4 lanes and an
+  // instruction 16 edges (quad record loads) over the doubled runs; the CAS pairs then carry
+  // half the slots each (Reddit k = 16 1.420 -> 1.375 ms, an 8-GPU shard 0.371 -> 0.365;
+  // at k = 24, 6 lanes per edge, +17 %: profiles/r05/bwd_two_slots_groups.jsonl)
+  if (o.bwd_features_per_lane == 0 && F == 4 && S == 2 && kF / S == 8) {
+    F = 2;
+    p->bwd_feats = F;
+  }
   p->bwd_slot_groups = S;
   p->bwd_kp = kF;
   p->bwd_ks = kF / S;  // accumulators per column and group (64-bit CAS pairs: unpadded)
