@@ -224,20 +224,24 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def spawn_ranks(n, argv, poll_s=0.2, grace_s=10.0):
+def spawn_ranks(n, argv, poll_s=0.2, grace_s=10.0, straggler_s=None):
     """`bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment): start N
     rank processes of this script with the torch.distributed.run environment (RANK,
     LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), relay rank 0's stdout
     (the JSON line), and return 0 when every rank exits 0. When a rank fails, the others
     (which may be waiting in a collective for it) are terminated by PID and the failing
-    rank's exit code is returned. This process imports neither torch nor maxk_kernels, so it
-    never initialises HIP before the children start (an exec or fork after HIP init is not
-    safe on this platform)."""
+    rank's exit code is returned. When some ranks exit 0 while others are still running
+    ``straggler_s`` seconds later (MAXK_BENCH_STRAGGLER_S, default 300: a rank stuck in a
+    collective its peers left), the rest are terminated and 124 is returned. This
+    process imports neither torch nor maxk_kernels, so it never initialises HIP before the
+    children start (an exec or fork after HIP init is not safe on this platform)."""
     import signal
     import subprocess
     import threading
 
     assert "torch" not in sys.modules, "the spawning parent must not import torch"
+    if straggler_s is None:
+        straggler_s = float(os.environ.get("MAXK_BENCH_STRAGGLER_S", "300"))
     port = os.environ.get("MASTER_PORT") or str(_free_port())
     base = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
                 ROLE_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
@@ -278,6 +282,7 @@ def spawn_ranks(n, argv, poll_s=0.2, grace_s=10.0):
         relay = threading.Thread(target=pump, args=(procs[0].stdout,), daemon=True)
         relay.start()
         rc = 0
+        first_done = None
         while True:
             codes = [p.poll() for p in procs]
             bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
@@ -289,6 +294,15 @@ def spawn_ranks(n, argv, poll_s=0.2, grace_s=10.0):
                 break
             if all(c == 0 for c in codes):
                 break
+            if first_done is None and any(c == 0 for c in codes):
+                first_done = time.time()
+            if first_done is not None and time.time() - first_done > straggler_s:
+                left = [i for i, c in enumerate(codes) if c is None]
+                print(f"[bench] ranks {left} still running {straggler_s:.0f}s after the others "
+                      f"exited; stopping them", file=sys.stderr, flush=True)
+                stop()
+                rc = 124
+                break
             time.sleep(poll_s)
     finally:
         stop()
@@ -298,16 +312,90 @@ def spawn_ranks(n, argv, poll_s=0.2, grace_s=10.0):
     return rc if rc >= 0 else 128 - rc
 
 
+def rank_identity(dev_index):
+    """This rank's device as the HIP runtime reports it (the driver checks these fields)."""
+    import socket
+    p = torch.cuda.get_device_properties(dev_index)
+    return {"rank": int(os.environ.get("RANK", "0")),
+            "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "host": socket.gethostname(), "device_index": dev_index,
+            "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "uuid": str(p.uuid), "name": p.name, "gcn_arch": p.gcnArchName,
+            "visible_devices": {v: os.environ[v] for v in ("HIP_VISIBLE_DEVICES",
+                                                           "ROCR_VISIBLE_DEVICES",
+                                                           "CUDA_VISIBLE_DEVICES")
+                                if v in os.environ}}
+
+
+def gather_topology(ident, backend, world):
+    """Every rank's identity (one all_gather_object), the group's world size and backend as
+    torch.distributed reports them, and the RCCL version torch is linked against."""
+    ranks = [ident]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, ident)
+    topo = {"world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
+            "launcher_world_size": world, "requested_backend": backend, "ranks": ranks,
+            "torch": torch.__version__, "hip": getattr(torch.version, "hip", None)}
+    try:
+        topo["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+    except Exception as exc:  # pragma: no cover - torch build without RCCL
+        topo["rccl_version"] = f"unavailable: {exc!r}"[:80]
+    return topo
+
+
+def check_topology(topo, backend):
+    """One GPU per rank under RCCL: two nccl ranks resolving to one device would time the same
+    GPU twice (or share it), so every rank refuses to run (non-zero exit)."""
+    if topo["world_size"] != topo["launcher_world_size"]:
+        raise SystemExit(f"[bench] torch.distributed world size {topo['world_size']} != "
+                         f"WORLD_SIZE {topo['launcher_world_size']}")
+    if backend != "nccl":
+        return
+    seen = {}
+    for r in topo["ranks"]:
+        for key in ((r["host"], "pci", r["pci_bus_id"]), (r["host"], "uuid", r["uuid"])):
+            if key in seen:
+                raise SystemExit(f"[bench] ranks {seen[key]} and {r['rank']} resolve to the same "
+                                 f"device ({key[1]} {key[2]} on {key[0]}): nccl needs one GPU "
+                                 f"per rank")
+            seen[key] = r["rank"]
+
+
 def _selftest_rank(spec):
     """MAXK_BENCH_SELFTEST (tests/test_bench_spawn.py): a rank that only reports what the
-    launcher handed it, without torch. 'ok': rank 0 prints one JSON line. 'fail:R': rank R
-    exits 3 and the others hang (as ranks stuck in a collective would)."""
+    launcher handed it, without HIP. 'ok': rank 0 prints one JSON line. 'fail:R': rank R
+    exits 3 and the others hang (as ranks stuck in a collective would). 'exit0:R': rank R
+    exits 0 at once and the others hang (the straggler limit ends them). 'topology' /
+    'topology:dup': the ranks form a gloo group, gather made-up device identities (distinct, or
+    all one device) and run the nccl one-GPU-per-rank check; rank 0 prints the topology."""
+    global torch, dist
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     if spec.startswith("fail:"):
         if rank == int(spec.split(":", 1)[1]):
             time.sleep(0.5)
             sys.exit(3)
         time.sleep(600)
+    if spec.startswith("exit0:"):
+        if rank == int(spec.split(":", 1)[1]):
+            sys.exit(0)
+        time.sleep(600)
+    if spec.startswith("topology"):
+        import torch as _torch
+        import torch.distributed as _dist
+        torch, dist = _torch, _dist
+        dist.init_process_group("gloo")
+        q = 0 if spec == "topology:dup" else rank
+        ident = {"rank": rank, "local_rank": int(os.environ["LOCAL_RANK"]), "host": "selftest",
+                 "device_index": q, "pci_bus_id": f"0000:{0x05 + q:02x}:00", "uuid": f"GPU-{q}",
+                 "name": "selftest", "gcn_arch": "gfx950", "visible_devices": {}}
+        topo = gather_topology(ident, "gloo", world)
+        check_topology(topo, "nccl")
+        if rank == 0:
+            print(json.dumps({"selftest": True, "topology": topo}), flush=True)
+        dist.destroy_process_group()
+        return
     if rank == 0:
         print(json.dumps({"selftest": True, "world": world, "rank": rank,
                           "local_rank": int(os.environ["LOCAL_RANK"]),
@@ -350,6 +438,9 @@ def run(args):
         else:
             dist.init_process_group("gloo")
         log(f"process group up ({backend}, world {world})")
+    # what RCCL actually sees: every rank's device, checked before any work
+    topology = gather_topology(rank_identity(dev_index), backend, world)
+    check_topology(topology, backend)
 
     n, e_target = graphs.DATASETS[args.dataset]
     d, k = args.dim, args.k
@@ -587,6 +678,7 @@ def run(args):
         "fwd_roofline_frac": fwd_gbs / HBM_PEAK_GBS,
         "bwd_roofline_frac": bwd_gbs / HBM_PEAK_GBS,
         "plan_build_s": plan_s,
+        "topology": topology,
         "cpu_baseline": None,
     }
 

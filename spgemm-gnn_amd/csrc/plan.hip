@@ -532,6 +532,12 @@ static int check_options(const maxk_plan_options& o) {
   MAXK_CHECK_ARG(o.bwd_unroll == 0 || o.bwd_unroll == 8 || o.bwd_unroll == 12 ||
                      o.bwd_unroll == 16,
                  "maxk_plan_create: bwd_unroll must be 0, 8, 12 or 16");
+  // the backward shapes that exist (spgemm.hip BWD_SHAPES): 16 waves x 8 sub-steps, 12 x 8 or
+  // 12, 8 x 8, 12 or 16 (an unroll with no kernel is refused, not replaced)
+  MAXK_CHECK_ARG(o.bwd_waves != 16 || o.bwd_unroll == 0 || o.bwd_unroll == 8,
+                 "maxk_plan_create: bwd_waves 16 runs bwd_unroll 8 only");
+  MAXK_CHECK_ARG(o.bwd_waves != 12 || o.bwd_unroll != 16,
+                 "maxk_plan_create: bwd_waves 12 runs bwd_unroll 8 or 12");
   MAXK_CHECK_REMOVED(o.bwd_order != 1, "bwd_order = 1 (heavy-first tasks)");
   MAXK_CHECK_ARG(o.bwd_order >= 0 && o.bwd_order <= 3, "maxk_plan_create: bwd_order must be 0, 2 or 3");
   MAXK_CHECK_ARG(o.bwd_slot_groups >= 0 && o.bwd_slot_groups <= 64 &&
@@ -1187,7 +1193,13 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
         const int64_t t = bS * c;
         return (double)t / ((double)((t + cus - 1) / cus) * cus);
       };
-      const int64_t lo = std::max<int64_t>(1, std::min(nch64, fl));
+      // the fill counts tasks, not edges: go below nch only while the blocks hold similar edge
+      // counts (largest <= 2x the mean), so a skewed block cannot become a one-round tail
+      // 
+      int64_t max_nnz = 0;
+      for (int b = 0; b < nblocks; ++b) max_nnz = std::max<int64_t>(max_nnz, offs[b + 1] - offs[b]);
+      const bool even_blocks = max_nnz * (int64_t)nblocks <= 2 * E;
+      const int64_t lo = even_blocks ? std::max<int64_t>(1, std::min(nch64, fl)) : nch64;
       int64_t hi = nch64;
       for (int64_t c = nch64 + 1; c <= nch64 + 2; ++c) {
         if ((double)E / ((double)nblocks * c) < 0.6 * kBwdMinTaskEdges) break;
@@ -1340,7 +1352,10 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   // static interleave (+2..3 % with the counter)
   p->bwd_handout = o.bwd_handout ? o.bwd_handout : 2;
   p->fwd_handout = o.fwd_handout ? o.fwd_handout : (k <= 16 || p->fwd_waves == 8 ? 2 : 1);
-  if (o.bwd_waves == 0) {
+  if (o.bwd_waves == 0 && (o.bwd_unroll == 12 || o.bwd_unroll == 16)) {
+    // an explicit unroll picks the waves that run it: 12 x 12, 8 x 16
+    p->bwd_waves = o.bwd_unroll == 12 ? 12 : 8;
+  } else if (o.bwd_waves == 0) {
     if (p->bwd_handout == 2 && !p->bwd_big) {
       // handed-out windows leave no wave a longer share than its neighbours, so more waves
       // only add latency hiding: 16 per work-group (Reddit k = 16 1.646 -> 1.504 ms, k = 64
@@ -1354,10 +1369,13 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       p->bwd_waves = 12;
     }
   }
-  // the unroll that actually launches: the 16-wave and > 4 GiB shapes run U = 8, 12 waves U =
-  // 8 or 12
-  if ((p->bwd_waves != 8 && !(p->bwd_waves == 12 && p->bwd_unroll == 12)) || p->bwd_big)
+  // the shape that actually launches: the 16-wave shape runs U = 8, 12 waves U
+  // = 8 or 12, and grad_out > 4 GiB (64-bit gathers) one shape, 8 waves x 8
+  if (p->bwd_waves != 8 && !(p->bwd_waves == 12 && p->bwd_unroll == 12)) p->bwd_unroll = 8;
+  if (p->bwd_big) {
+    p->bwd_waves = 8;
     p->bwd_unroll = 8;
+  }
   if (!btasks.empty()) {
     PLAN_TRY(hipMalloc(&p->bwd_tasks, sizeof(BwdTask) * btasks.size()));
     PLAN_TRY(hipMemcpyAsync(p->bwd_tasks, btasks.data(), sizeof(BwdTask) * btasks.size(),
@@ -1455,6 +1473,15 @@ extern "C" int maxk_plan_get_info_sized(const maxk_plan* p, maxk_plan_info* out,
   info.fwd_unroll = p->fwd_unroll;
   info.bwd_waves = p->bwd_twopass ? 0 : p->bwd_waves;  // the two-pass kernels have one shape
   info.bwd_unroll = p->bwd_twopass ? 0 : p->bwd_unroll;
+  if (p->fwd_chunk3) {
+    info.fwd_layout = 2;
+    info.fwd_record_bytes = p->fwd_rec_bytes;
+  } else if (p->dim_k % 4 != 0) {
+    info.fwd_layout = 3;
+  } else if (!p->fwd_two_tables) {
+    info.fwd_layout = 1;
+    info.fwd_record_bytes = p->fwd_rec_bytes;
+  }
   std::memcpy(out, &info, (size_t)std::min<int64_t>(info_bytes, (int64_t)sizeof(maxk_plan_info)));
   return MAXK_OK;
 }

@@ -30,6 +30,7 @@ from .ops import (  # noqa: F401
 from .autograd import (  # noqa: F401
     CSRGraph,
     DenseAggFunction,
+    MaxKAggregateFunction,
     MaxKFunction,
     SpGEMMFunction,
     dense_aggregate,
@@ -52,7 +53,7 @@ from .layers import (  # noqa: F401,E402
 __all__ = [
     "maxk_forward", "maxk_backward", "spgemm_forward", "spgemm_backward",
     "dense_spmm", "cbsr_stats", "plan_col_order", "GraphPlan", "get_plan", "clear_plan_cache", "CSRGraph",
-    "MaxKFunction", "SpGEMMFunction", "maxk", "spgemm", "maxk_aggregate", "MaxKError",
+    "MaxKFunction", "MaxKAggregateFunction", "SpGEMMFunction", "maxk", "spgemm", "maxk_aggregate", "MaxKError",
     "densify", "MaxKSAGEConv", "MaxKGCNConv", "MaxKGINConv", "MaxKSAGE", "MaxKGCN",
     "MaxKGIN", "dense_aggregate", "DenseAggFunction",
 ]

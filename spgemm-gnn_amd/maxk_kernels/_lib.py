@@ -27,7 +27,10 @@ SIGNATURES = {
     "maxk_topk_cbsr_count": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "maxk_topk_cbsr_tables": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32,
                                              _i32, _vp]),
+    "maxk_topk_cbsr_ex": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32,
+                                         _i32, _vp]),
     "maxk_scatter_backward": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
+    "maxk_scatter_backward_tables": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
     "maxk_plan_create": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp,
                                         ctypes.POINTER(_vp)]),
     "maxk_plan_create_rect": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32,
@@ -66,6 +69,10 @@ SIGNATURES = {
     "maxk_dense_spmm_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),
     "maxk_warp4_build": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
 }
+
+
+# maxk_topk_cbsr_ex's stats buffer (uint32 words; the pair is words 0-1, the rest scratch)
+TOPK_STATS_WORDS = 8194
 
 
 class PlanOptions(ctypes.Structure):
@@ -157,6 +164,9 @@ class PlanInfo(ctypes.Structure):
         ("fwd_unroll", _i32),
         ("bwd_waves", _i32),
         ("bwd_unroll", _i32),
+        # ABI 4
+        ("fwd_layout", _i32),
+        ("fwd_record_bytes", _i32),
     ]
 
     def as_dict(self):

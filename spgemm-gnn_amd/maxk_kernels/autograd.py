@@ -156,6 +156,21 @@ class CSRGraph:
         return g
 
 
+def _mask_padding(grad_data, sp_index, count):
+    """ref_compat rows fill ``count`` < k slots; the padding slots (0.0f, 0) carry no gradient:
+    each is pointed at the row's last filled slot with that slot's gradient, so the scatter
+    (last slot wins) never writes into a feature 0 that was not selected."""
+    count = count.to(torch.int64)
+    k = sp_index.shape[1]
+    pad = torch.arange(k, device=count.device)[None, :] >= count[:, None]
+    last = (count - 1).clamp(min=0)[:, None]
+    g_last = torch.where(count[:, None] > 0, grad_data.gather(1, last),
+                         torch.zeros_like(grad_data[:, :1]))
+    sp_index = torch.where(pad, sp_index.gather(1, last), sp_index).contiguous()
+    grad_data = torch.where(pad, g_last, grad_data).contiguous()
+    return grad_data, sp_index
+
+
 class MaxKFunction(torch.autograd.Function):
     """x [N, D] -> CBSR (sp_data, sp_index); backward = the device scatter of grad_data
     into the selected features (the ``grad * mask`` of utils/models.py:23-26).
@@ -185,14 +200,7 @@ class MaxKFunction(torch.autograd.Function):
         sp_index = saved[0]
         grad_data = grad_data.contiguous()
         if len(saved) == 2:
-            count = saved[1].to(torch.int64)
-            k = sp_index.shape[1]
-            pad = torch.arange(k, device=count.device)[None, :] >= count[:, None]
-            last = (count - 1).clamp(min=0)[:, None]
-            g_last = torch.where(count[:, None] > 0, grad_data.gather(1, last),
-                                 torch.zeros_like(grad_data[:, :1]))
-            sp_index = torch.where(pad, sp_index.gather(1, last), sp_index).contiguous()
-            grad_data = torch.where(pad, g_last, grad_data).contiguous()
+            grad_data, sp_index = _mask_padding(grad_data, sp_index, saved[1])
         grad_x = ops.maxk_backward(grad_data, sp_index, dim_origin=ctx.dim_origin)
         return grad_x, None, None
 
@@ -245,6 +253,43 @@ class DenseAggFunction(torch.autograd.Function):
         return grad_x, None
 
 
+class MaxKAggregateFunction(torch.autograd.Function):
+    """``A @ densify(MaxK(x))`` as one producer-consumer pair (utils/maxk_layers.py:16-34:
+    MaxK feeding the SpGEMM). The top-k writes the CBSR features straight into the layout
+    the plan's forward gathers (its packed records when ``fwd_layout`` is 1, GraphPlan.new_cbsr)
+    together with the fixed-point statistics of the emitted rows (maxk_topk_cbsr_ex), so the
+    forward launches no per-call pack or statistics pass. Backward: the SSpMM on the same plan
+    (selectors read at the record stride), then the MaxK scatter (same rules as MaxKFunction
+    for ref_compat padding)."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, graph: CSRGraph, k: int, mode: str = "exact"):
+        x = x.contiguous()
+        d = x.shape[1]
+        plan = graph.plan(d, k)
+        sp_data, sp_index = plan.new_cbsr()
+        stats = ops.topk_stats_buffer(x.device)
+        res = ops.maxk_forward(x, k, mode=mode, return_index=True, out=(sp_data, sp_index),
+                               stats=stats, return_count=mode != "exact")
+        out = plan.forward(sp_data, sp_index, stats=stats[:2].view(1, 2))
+        ctx.save_for_backward(sp_index, *res[2:])
+        ctx.plan = plan
+        ctx.dim_origin = d
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        saved = ctx.saved_tensors
+        sp_index = saved[0]
+        grad_x = None
+        if ctx.needs_input_grad[0]:
+            grad_sp = ctx.plan.backward(grad_out.contiguous(), sp_index)
+            if len(saved) == 2:
+                grad_sp, sp_index = _mask_padding(grad_sp, sp_index, saved[1])
+            grad_x = ops.maxk_backward(grad_sp, sp_index, dim_origin=ctx.dim_origin)
+        return grad_x, None, None, None
+
+
 def dense_aggregate(x: torch.Tensor, graph: CSRGraph) -> torch.Tensor:
     """Y = A @ x for dense x (ReLU layers), differentiable in x."""
     return DenseAggFunction.apply(x, graph)
@@ -272,6 +317,6 @@ def spgemm(sp_data: torch.Tensor, sp_index: torch.Tensor, graph: CSRGraph,
 def maxk_aggregate(x: torch.Tensor, graph: CSRGraph, k: int, mode: str = "exact",
                    ) -> torch.Tensor:
     """Fused MaxK + aggregation: ``A @ (x * topk_mask(x))`` (DGL: MaxK.apply then
-    update_all(u_mul_e, sum) with edge weights ``graph.val``)."""
-    sp_data, sp_index = maxk(x, k, mode)
-    return spgemm(sp_data, sp_index, graph, x.shape[1])
+    update_all(u_mul_e, sum) with edge weights ``graph.val``), differentiable in x; the
+    top-k hands the forward its records and statistics (MaxKAggregateFunction)."""
+    return MaxKAggregateFunction.apply(x, graph, k, mode)

@@ -43,7 +43,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .autograd import CSRGraph, dense_aggregate, densify, maxk, spgemm
+from .autograd import CSRGraph, dense_aggregate, densify, maxk, maxk_aggregate, spgemm
 
 NONLINEAR = ("maxk", "relu")
 
@@ -120,9 +120,12 @@ class MaxKSAGEConv(nn.Module):
         elif self.maxk_after_fc:
             # reference ordering (maxk_layers.py:85-88): MaxK(fc_neigh(feat)) aggregated
             h_self = self.fc_self(feat)
-            sp_data, sp_index = maxk(self.fc_neigh(feat), self.maxk, self.topk_mode)
-            sp_data = _sparse_dropout(sp_data, self.feat_drop, self.training)
-            rst = h_self + spgemm(sp_data, sp_index, csr, self.out_feats)
+            if self.feat_drop > 0 and self.training:
+                sp_data, sp_index = maxk(self.fc_neigh(feat), self.maxk, self.topk_mode)
+                sp_data = _sparse_dropout(sp_data, self.feat_drop, self.training)
+                rst = h_self + spgemm(sp_data, sp_index, csr, self.out_feats)
+            else:  # no dropout between MaxK and the SpGEMM: the fused producer-consumer pair
+                rst = h_self + maxk_aggregate(self.fc_neigh(feat), csr, self.maxk, self.topk_mode)
         else:
             sp_data, sp_index = maxk(feat, self.maxk, self.topk_mode)
             sp_data = _sparse_dropout(sp_data, self.feat_drop, self.training)
@@ -174,10 +177,12 @@ class MaxKGCNConv(nn.Module):
         if self.nonlinear == "relu":
             x = F.dropout(feat, self.feat_drop, self.training) if self.feat_drop > 0 else feat
             rst = dense_aggregate(x, csr.with_values(self.norm))
-        else:
+        elif self.feat_drop > 0 and self.training:
             sp_data, sp_index = maxk(feat, self.maxk, self.topk_mode)
             sp_data = _sparse_dropout(sp_data, self.feat_drop, self.training)
             rst = spgemm(sp_data, sp_index, csr.with_values(self.norm), feat.shape[1])
+        else:
+            rst = maxk_aggregate(feat, csr.with_values(self.norm), self.maxk, self.topk_mode)
         if self.bias is not None:
             rst = rst + self.bias
         return rst

@@ -25,7 +25,8 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import ACC_KINDS, BWD_ALGOS, COL_ORDERS, PlanInfo, PlanOptions, check, lib
+from ._lib import (ACC_KINDS, BWD_ALGOS, COL_ORDERS, TOPK_STATS_WORDS, PlanInfo, PlanOptions,
+                   check, lib)
 
 TOPK_MODES = {"exact": 0, "ref_compat": 1}
 
@@ -74,7 +75,8 @@ def _table(t: torch.Tensor, name: str, dtype: torch.dtype, rows: int, k: int) ->
 # MaxK top-k
 # -------------------------------------------------------------------------------------
 def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
-                 return_index: bool = False, out=None, return_count: bool = False):
+                 return_index: bool = False, out=None, return_count: bool = False,
+                 stats: Optional[torch.Tensor] = None):
     """MaxK nonlinearity -> CBSR. Reference: ``maxk_forward(input, k) -> [N, k] f32``.
 
     Checks (bindings.cpp:27-30): "input must be a CUDA tensor", "input must be
@@ -87,6 +89,11 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
     :class:`maxk_kernels.dist.ShardedAggregation`). ``return_count=True``
     appends the int32 ``[N]`` number of filled slots per row (``k`` in exact mode; in
     ref_compat mode the slots past it are the reference's ``(0.0f, 0)`` padding).
+    ``stats``: a contiguous int32 CUDA tensor of :func:`topk_stats_buffer`'s size whose first
+    two elements receive the fixed-point statistics of the emitted table with the top-k
+    (``maxk_topk_cbsr_ex``; the rest is the launch's scratch): the pair
+    :meth:`GraphPlan.forward` takes as ``stats=stats[:2].view(1, 2)`` instead of its own pass
+    over the table.
     """
     _need(input.is_cuda, "input must be a CUDA tensor")
     _need(input.is_contiguous(), "input must be contiguous")
@@ -107,14 +114,24 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
         ds = _table(sp_data, "out[0]", torch.float32, n, k)
         is_ = _table(sp_index, "out[1]", torch.uint8, n, k)
     count = torch.empty(n, dtype=torch.int32, device=input.device) if return_count else None
+    if stats is not None:
+        _need(stats.is_cuda and stats.device == input.device and stats.is_contiguous() and
+              stats.dtype == torch.int32 and stats.numel() >= TOPK_STATS_WORDS,
+              f"stats must be a contiguous int32 CUDA tensor of {TOPK_STATS_WORDS} elements on "
+              f"the input's device (topk_stats_buffer)")
     with _device(input.device):
-        check(lib.maxk_topk_cbsr_tables(_p(input), _p(sp_data), ds, _p(sp_index), is_,
-                                        _p(count), n, d, k, TOPK_MODES[mode], _stream()),
+        check(lib.maxk_topk_cbsr_ex(_p(input), _p(sp_data), ds, _p(sp_index), is_, _p(count),
+                                    _p(stats), n, d, k, TOPK_MODES[mode], _stream()),
               "maxk_forward")
     res = (sp_data, sp_index) if return_index else (sp_data,)
     if return_count:
         res = res + (count,)
     return res if len(res) > 1 else res[0]
+
+
+def topk_stats_buffer(device) -> torch.Tensor:
+    """The ``stats=`` buffer of :func:`maxk_forward` (MAXK_TOPK_STATS_WORDS int32)."""
+    return torch.empty(TOPK_STATS_WORDS, dtype=torch.int32, device=device)
 
 
 def maxk_backward(grad_output: torch.Tensor, indices: torch.Tensor,
@@ -131,20 +148,26 @@ def maxk_backward(grad_output: torch.Tensor, indices: torch.Tensor,
     _need(grad_output.is_contiguous(), "grad_output must be contiguous")
     _need(grad_output.dim() == 2, "grad_output must be 2D tensor")
     _need(indices.is_cuda, "indices must be a CUDA tensor")
-    _need(indices.is_contiguous(), "indices must be contiguous")
     _need(indices.shape == grad_output.shape, "indices must have the shape of grad_output")
     _need(grad_output.dtype == torch.float32, "grad_output must be float32")
     n, k = grad_output.shape
+    # u8 selectors may be row-strided (the interleaved records of maxk_aggregate); other
+    # integer dtypes are converted (contiguous)
+    strided_u8 = (indices.dtype == torch.uint8 and indices.dim() == 2 and
+                  (n <= 1 or indices.stride(1) == 1) and (n <= 1 or indices.stride(0) >= k))
+    _need(indices.is_contiguous() or strided_u8, "indices must be contiguous")
     if indices.dtype != torch.uint8:
         _need(not indices.dtype.is_floating_point, "indices must be an integer tensor")
         indices = indices.to(torch.uint8)
+    istride = indices.stride(0) if n > 1 else k
     if dim_origin is None:
         dim_origin = int(indices.max().item()) + 1 if indices.numel() else 1
     _need(1 <= k <= dim_origin <= 256, "k must be between 1 and input dimension")
     grad_in = torch.empty((n, dim_origin), dtype=torch.float32, device=grad_output.device)
     with _device(grad_output.device):
-        check(lib.maxk_scatter_backward(_p(grad_output), _p(indices), _p(grad_in), n,
-                                        dim_origin, k, _stream()), "maxk_backward")
+        check(lib.maxk_scatter_backward_tables(_p(grad_output), _p(indices), istride,
+                                               _p(grad_in), n, dim_origin, k, _stream()),
+              "maxk_backward")
     return grad_in
 
 
@@ -332,6 +355,23 @@ class GraphPlan:
     @property
     def device_bytes(self) -> int:
         return int(self.info()["device_bytes"])
+
+    def new_cbsr(self):
+        """Uninitialised ``(sp_data, sp_index)`` [num_cols, k] tables in the layout this plan's
+        forward gathers (``fwd_layout``): strided views of one buffer of packed records
+        (``fwd_record_bytes`` per column, values then selectors) when the forward reads packed
+        records, so a top-k written there (:func:`maxk_forward` ``out=``) needs no per-call
+        pack; two plain tables otherwise."""
+        layout = getattr(self, "_layout", None)
+        if layout is None:
+            info = self.info()
+            layout = self._layout = (info["fwd_layout"], info["fwd_record_bytes"])
+        n, k = self.num_cols, self.dim_k
+        if layout[0] == 1 and n > 0:
+            rec = torch.empty((n, layout[1]), dtype=torch.uint8, device=self.device)
+            return rec[:, :4 * k].view(torch.float32), rec[:, 4 * k:5 * k]
+        return (torch.empty((n, k), dtype=torch.float32, device=self.device),
+                torch.empty((n, k), dtype=torch.uint8, device=self.device))
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -15,10 +15,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
 
 
-def _run(n, spec, timeout=60):
+def _run(n, spec, timeout=60, extra_env=None):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR")}
     env["MAXK_BENCH_SELFTEST"] = spec
+    env.update(extra_env or {})
     t0 = time.time()
     p = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--steps", "3"], env=env,
                        capture_output=True, text=True, timeout=timeout)
@@ -76,3 +77,36 @@ def test_launcher_env_runs_as_a_rank():
     rec = json.loads(p.stdout.strip())
     assert rec["spawned"] is False and rec["world"] == 2
     assert "spawning" not in p.stderr
+
+
+def test_straggler_limit_ends_ranks_left_behind():
+    """rank 1 exits 0 while rank 0 hangs (as in a collective its peer left); the
+    parent stops it after MAXK_BENCH_STRAGGLER_S and fails the job with 124."""
+    p, dt = _run(2, "exit0:1", extra_env={"MAXK_BENCH_STRAGGLER_S": "2"})
+    assert p.returncode == 124, (p.returncode, p.stderr)
+    assert dt < 30, dt
+    assert "still running" in p.stderr
+
+
+def test_topology_gathered_from_every_rank():
+    """rank 0's line carries torch.distributed's world size and backend,
+    every rank's device identity (all-gathered) and the RCCL version (selftest ranks: a gloo
+    group with made-up, distinct device identities)."""
+    p, _ = _run(3, "topology", timeout=120)
+    assert p.returncode == 0, p.stderr
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]   # gloo logs its own
+    assert len(line) == 1, p.stdout
+    topo = json.loads(line[0])["topology"]
+    assert topo["world_size"] == 3 and topo["launcher_world_size"] == 3
+    assert topo["backend"] == "gloo"
+    assert [r["rank"] for r in topo["ranks"]] == [0, 1, 2]
+    assert len({r["pci_bus_id"] for r in topo["ranks"]}) == 3
+    assert topo["rccl_version"].count(".") == 2
+
+
+def test_two_nccl_ranks_on_one_device_are_refused():
+    """Two ranks whose identities resolve to one device fail the one-GPU-per-rank check that
+    every nccl run makes before any work: non-zero exit, the reason on stderr."""
+    p, _ = _run(2, "topology:dup", timeout=120)
+    assert p.returncode != 0, p.stdout
+    assert "resolve to the same device" in p.stderr

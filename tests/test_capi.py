@@ -25,7 +25,7 @@ def declared_functions():
 def test_library_is_in_tree_and_loaded():
     assert os.path.exists(_lib.LIB_PATH)
     assert _lib.LIB_PATH.startswith(os.path.join(ROOT, "spgemm-gnn_amd"))
-    assert maxk_kernels.ABI_VERSION == 3
+    assert maxk_kernels.ABI_VERSION == 4
 
 
 def test_exports_every_declared_symbol():

@@ -5,11 +5,11 @@
   kernel on the transposed CSR backward) on the Flickr-shaped graph (N=89,250,
   E=989,006 + self-loops, synthetic), hidden 64, checked against the oracle's DGL
   update_all(copy_u, mean) restatement, plus a MaxKSAGE(nonlinear='relu') training step;
-* config 5 — "Reddit row-partitioned across 8 x MI355X": the full-size W=8 RowPartition with
+* config 5 — "Reddit row-partitioned across 8 x MI355X": the full-size RowPartition with
   every rank's rectangular plans run on this one GPU and the all-gather / reduce-scatter
   emulated with tensor ops (the real collectives are covered by tests/test_dist.py over
-  gloo and test_gpu_dist.py over RCCL), checked by the adjoint identity, linearity against
-  the single-GPU plan and oracle-sampled rows and columns.
+  gloo and test_gpu_dist.py over RCCL), for W in {2, 4, 8} and k in {16, 64}: every row of
+  the forward and every column of the backward against the oracle, plus the adjoint identity.
 """
 import time
 
@@ -92,48 +92,45 @@ def test_config1_flickr_relu_sage_trains(gpu):
     assert np.isfinite(losses).all() and losses[-1] < losses[0]
 
 
-def _sampled_rows_ok(y, ptr, idx, val, sp_data, sp_index, D, nrows=1500, seed=0):
-    N = ptr.numel() - 1
-    p = ptr.cpu().numpy()
-    deg = np.diff(p)
-    rows = np.unique(np.concatenate([np.random.RandomState(seed).choice(N, nrows, replace=False),
-                                     np.argsort(deg)[-8:]]))
-    ix, v = idx.cpu().numpy(), val.cpu().numpy()
-    sub_ptr = np.zeros(N + 1, np.int32)
-    sub_ptr[1:rows.size + 1] = np.cumsum(deg[rows])
-    sub_ptr[rows.size + 1:] = sub_ptr[rows.size]
-    sub_idx = np.concatenate([ix[p[r]:p[r + 1]] for r in rows])
-    sub_val = np.concatenate([v[p[r]:p[r + 1]] for r in rows])
-    ref, mag = oracle.spgemm_forward(sub_ptr, sub_idx, sub_val, sp_data.cpu().numpy(),
-                                     sp_index.cpu().numpy(), D, with_mag=True)
-    got = y[torch.from_numpy(rows).to(y.device)].cpu().numpy()
-    return oracle.close_enough(got, ref[:rows.size], mag[:rows.size])
+_ORACLE5 = {}
 
 
-def _sampled_cols_ok(gs, ptr, idx, val, sp_index, g, ncols=400, seed=1):
-    N, K = sp_index.shape
-    cols = np.random.RandomState(seed).choice(N, ncols, replace=False)
-    ix = idx.cpu().numpy()
-    e_ids = np.nonzero(np.isin(ix, cols))[0]
-    rows_of = np.repeat(np.arange(N), np.diff(ptr.cpu().numpy()))[e_ids]
-    c = ix[e_ids]
-    v = val.cpu().numpy()[e_ids].astype(np.float64)
-    si = sp_index.cpu().numpy()
-    terms = v[:, None] * g.cpu().numpy()[rows_of[:, None], si[c].astype(np.int64)]
-    ref = np.zeros((N, K))
-    mag = np.zeros((N, K))
-    np.add.at(ref, c, terms)
-    np.add.at(mag, c, np.abs(terms))
-    return oracle.close_enough(gs.cpu().numpy()[cols], ref[cols], mag[cols])
+def _config5_oracle(ptr, sp_data, sp_index, g, k, D):
+    """The whole-graph oracle outputs (f64 sums and |terms| sums) for config 5 at this k,
+    computed once and shared by the world sizes."""
+    if _ORACLE5.get("k") != k:
+        _ORACLE5.clear()
+        idx = graphs.synthetic_rows(ptr, seed=97)
+        val = graphs.sage_mean_values(ptr, num_edges=idx.numel())
+        p, ix, v = ptr.cpu().numpy(), idx.cpu().numpy(), val.cpu().numpy()
+        del idx, val
+        si = sp_index.cpu().numpy()
+        fwd = oracle.spgemm_forward(p, ix, v, sp_data.cpu().numpy(), si, D, with_mag=True)
+        bwd = oracle.sspmm_backward(p, ix, v, g.cpu().numpy(), si, with_mag=True)
+        _ORACLE5.update(k=k, fwd=fwd, bwd=bwd)
+    return _ORACLE5["fwd"], _ORACLE5["bwd"]
 
 
-@pytest.mark.parametrize("k", [16])
-def test_config5_reddit_w8_partition(gpu, k):
-    """BASELINE config 5 emulated on one GPU: the bench graph (each rank generates only its
-    rows), every rank's ShardedAggregation over the all-gathered record table (filled here as
-    the one RCCL all-gather would, statistics pairs included), the reduce-scatter as a sum."""
+def _close_in_chunks(got, ref, mag, rows=1 << 17):
+    worst = 0.0
+    for a in range(0, ref.shape[0], rows):
+        ok, w = oracle.close_enough(got[a:a + rows], ref[a:a + rows], mag[a:a + rows])
+        worst = max(worst, w)
+        assert ok, (a, w)
+    return worst
+
+
+@pytest.mark.parametrize("k", [16, 64])
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_config5_reddit_partition(gpu, W, k):
+    """BASELINE config 5 emulated on one GPU, the path the 8-GPU bench times: the bench graph
+    (each rank generates only its rows), every rank's ShardedAggregation over the all-gathered
+    record table (filled here as the one RCCL all-gather would, statistics pairs included), the
+    reduce-scatter as a sum. EVERY row of the forward and EVERY column of the backward against
+    the oracle's whole-graph f64 sums (oracle.close_enough: 1e-5 relative, 1e-5 of the |terms|
+    sum where terms cancel), the worst error/bound printed per (W, k)."""
     from maxk_kernels.dist import ShardedAggregation, record_bytes, record_views
-    D, W = 256, 8
+    D = 256
     n, e = graphs.DATASETS["reddit"]
     ptr = graphs.synthetic_ptr(n, e, seed=97, device=gpu)
     h = graphs.features(n, D, seed=97, device=gpu)
@@ -167,6 +164,7 @@ def test_config5_reddit_w8_partition(gpu, k):
         del shard
     torch.cuda.synchronize()
     gs = torch.cat([grad_table[part.table_positions(q, gpu)] for q in range(W)])
+    del grad_table, table_rec
     # nnz balance of the partition: every rank within 1 % of E / W
     assert max(ranks_e) <= 1.01 * e / W and sum(ranks_e) == e
     # adjoint identity <A densify(sp), G> = <sp, SSpMM(G)>
@@ -174,16 +172,9 @@ def test_config5_reddit_w8_partition(gpu, k):
     rhs = (sp_data.double() * gs.double()).sum().item()
     scale = (y.double().abs() * g.double().abs()).sum().item()
     assert abs(lhs - rhs) <= 1e-5 * scale
-    # the single-GPU plan on the whole graph gives the same sums
-    idx = graphs.synthetic_rows(ptr, seed=97)
-    val = graphs.sage_mean_values(ptr, num_edges=e)
-    y1, _ = mk.spgemm_forward(ptr, idx, val, sp_data, sp_index, n, e, k, D)
-    g1 = mk.spgemm_backward(ptr, idx, val, g, sp_index, n, e, k, D)
-    assert ((y - y1).abs() <= 2e-5 * y1.abs().max()).all()
-    assert ((gs - g1).abs() <= 2e-5 * g1.abs().max()).all()
-    del y1, g1
+    (ref, mag), (gref, gmag) = _config5_oracle(ptr, sp_data, sp_index, g, k, D)
+    wf = _close_in_chunks(y.cpu().numpy(), ref, mag)
+    wb = _close_in_chunks(gs.cpu().numpy(), gref, gmag)
+    print(f"config 5 reddit W={W} k={k}: forward every row worst err/bound {wf:.3g}; "
+          f"backward every column worst err/bound {wb:.3g}")
     mk.clear_plan_cache()
-    ok, worst = _sampled_rows_ok(y, ptr, idx, val, sp_data, sp_index, D)
-    assert ok, worst
-    ok, worst = _sampled_cols_ok(gs, ptr, idx, val, sp_index, g)
-    assert ok, worst

@@ -90,6 +90,21 @@ def test_topk_ref_compat_edge_rows_bit_exact(gpu, k):
     assert np.array_equal(d.cpu().numpy().view(np.uint32), gd.view(np.uint32))
 
 
+NAN_ROWS = os.path.join(os.path.dirname(__file__), "golden", "maxk_exact_nan.npz")
+
+
+@pytest.mark.parametrize("k", [1, 8, 16, 32, 64])
+def test_topk_exact_nan_rows_bit_exact(gpu, k):
+    """Exact mode on +-NaN rows (tests/golden/make_golden.py:nan_rows): every NaN ranks above
+    +Inf, NaNs tie at the lowest index, as torch.topk (tests/test_oracle.py checks the fixture
+    against it); bit for bit, NaN payloads included, in the plain and the record layouts."""
+    with np.load(NAN_ROWS, allow_pickle=False) as z:
+        x, gd, gi = z["x"], z[f"data_k{k}"], z[f"index_k{k}"]
+    d, i = mk.maxk_forward(to_dev(x, gpu), k, mode="exact", return_index=True)
+    assert np.array_equal(i.cpu().numpy(), gi)
+    assert np.array_equal(d.cpu().numpy().view(np.uint32), gd.view(np.uint32))
+
+
 @pytest.mark.parametrize("k", [8, 16, 24, 32, 64])
 @pytest.mark.parametrize("mode", ["exact", "ref_compat"])
 def test_topk_golden_bit_exact(gpu, golden, k, mode):
@@ -896,3 +911,108 @@ def test_ref_compat_padding_slots_carry_no_gradient(gpu):
             if od[r, j] != 0 or (j == 0 and x[r, oi[r, 0]] > 0):   # a filled slot
                 expect[r, oi[r, j]] = wn[r, j]
     assert np.array_equal(xt.grad.cpu().numpy(), expect)
+
+
+# ------------------------------------------------------------ fused top-k -> forward (round 6)
+def _stat_rows(n, d, seed):
+    """Random rows plus rows whose statistics are special: all zero, +-Inf, NaN of both signs,
+    denormals, a single spike (ref_compat fills one slot and pads the rest)."""
+    x = graphs.features(n, d, seed=seed)
+    x[3] = 0.0
+    x[4, 7] = float("inf")
+    x[5, 9] = -float("inf")
+    x[6, 11] = float("nan")
+    x[7] = torch.from_numpy(np.array([0xffc00000] * d, np.uint32).view(np.float32))
+    x[8] = 1e-40
+    x[9, 100] = 1e6
+    return x
+
+
+@pytest.mark.parametrize("k", [1, 8, 16, 24, 32, 64])
+@pytest.mark.parametrize("mode", ["exact", "ref_compat"])
+@pytest.mark.parametrize("records", [False, True])
+def test_topk_fused_stats_equal_cbsr_stats(gpu, k, mode, records):
+    """maxk_topk_cbsr_ex (stats=): the pair fused into the top-k equals maxk_cbsr_stats over
+    the emitted table bit for bit, and the table equals the plain top-k's, on random rows and
+    rows with zeros, +-Inf, +-NaN, denormals and ref_compat padding (the special rows one at a
+    time, so each sets the pair), in the plain and the 128-B record layouts."""
+    n, d = 3000, 256
+    base = graphs.features(n, d, seed=k)
+    special = _stat_rows(16, d, seed=k + 1)
+    for r in [None] + list(range(3, 10)):
+        x = base.clone()
+        if r is not None:
+            x[1234] = special[r]
+        xd = x.to(gpu)
+        if records:
+            rb = max(128, -(-5 * k // 16) * 16)
+            rec = torch.empty((n, rb), dtype=torch.uint8, device=gpu)
+            sd, si = rec[:, :4 * k].view(torch.float32), rec[:, 4 * k:5 * k]
+            if k % 4:
+                pytest.skip("records need k % 4 == 0")
+        else:
+            sd = torch.empty((n, k), device=gpu)
+            si = torch.empty((n, k), dtype=torch.uint8, device=gpu)
+        st = mk.ops.topk_stats_buffer(gpu).fill_(-1)
+        mk.maxk_forward(xd, k, mode=mode, return_index=True, out=(sd, si), stats=st)
+        ref = mk.cbsr_stats(sd, si)
+        assert st[:2].tolist() == ref.view(-1).tolist(), (r, st[:2].tolist(), ref.tolist())
+        d0, i0 = mk.maxk_forward(xd, k, mode=mode, return_index=True)
+        assert torch.equal(si.cpu(), i0.cpu())
+        assert np.array_equal(sd.cpu().numpy().view(np.uint32), d0.cpu().numpy().view(np.uint32))
+
+
+def test_topk_fused_stats_empty_and_tiny(gpu):
+    """N = 0 writes the all-zero pair (the forward then takes f64); N = 1 and N = 5."""
+    st = mk.ops.topk_stats_buffer(gpu).fill_(7)
+    x = torch.empty((0, 64), device=gpu)
+    mk.maxk_forward(x, 8, return_index=True, stats=st)
+    assert st[:2].tolist() == [0, 0]
+    for n in (1, 5):
+        x = graphs.features(n, 64, seed=n).to(gpu)
+        sd, si = mk.maxk_forward(x, 8, return_index=True, stats=st)
+        assert st[:2].tolist() == mk.cbsr_stats(sd, si).view(-1).tolist()
+    with pytest.raises(RuntimeError, match="stats must be"):
+        mk.maxk_forward(x, 8, return_index=True, stats=st[:2])
+
+
+@pytest.mark.parametrize("k", [8, 16, 24, 32, 64])
+@pytest.mark.parametrize("mode", ["exact", "ref_compat"])
+def test_maxk_aggregate_fused_equals_unfused(gpu, k, mode):
+    """maxk_aggregate (top-k writing the forward's layout and statistics, no pack or statistics
+    pass) against MaxKFunction -> SpGEMMFunction and the oracle: the output equals the unfused
+    one bitwise where the forward is fixed point (k >= 16: integer sums, the same statistics);
+    both outputs and both input gradients within the oracle bound (the backward's f32 LDS
+    accumulation order varies from run to run); plan layouts covered: lane chunks (k = 8, 24),
+    packed records (16), two tables (32, 64)."""
+    pt, it = graphs.synthetic_csr(2000, 300_000, seed=37)   # 150 edges per column: k = 16
+    p, ix, v = pt.numpy(), it.numpy(), graphs.sage_mean_values(pt).numpy()  # packs records
+    n, d = p.size - 1, 256
+    x = graphs.features(n, d, seed=31 + k)
+    x[::7, 5] = 1e6                          # ref_compat: single-hit rows with padding slots
+    g = graphs.features(n, d, seed=32 + k).to(gpu)
+    graph = mk.CSRGraph(*graph_on(gpu, p, ix, v))
+    layout = graph.plan(d, k).info()["fwd_layout"]
+    assert layout == {8: 2, 24: 2, 16: 1, 32: 0, 64: 0}[k]
+    x1 = x.to(gpu).requires_grad_(True)
+    y1 = mk.maxk_aggregate(x1, graph, k, mode)
+    y1.backward(g)
+    x2 = x.to(gpu).requires_grad_(True)
+    sd, si = mk.maxk(x2, k, mode)
+    y2 = mk.spgemm(sd, si, graph, d)
+    y2.backward(g)
+    if k >= 16:
+        assert torch.equal(y1, y2)
+    od, oi = oracle.maxk(x.numpy(), k, mode)
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    assert_close(y1, ref, mag)
+    assert_close(y2, ref, mag)
+    gs, gmag = oracle.sspmm_backward(p, ix, v, g.cpu().numpy(), oi, with_mag=True)
+    filled = od != 0 if mode == "ref_compat" else np.ones_like(od, bool)
+    gx_ref = np.zeros((n, d))
+    gx_mag = np.zeros((n, d))
+    rows = np.repeat(np.arange(n)[:, None], k, 1)
+    gx_ref[rows[filled], oi[filled]] = gs[filled]      # ascending unique selectors per row
+    gx_mag[rows[filled], oi[filled]] = gmag[filled]
+    assert_close(x1.grad, gx_ref, gx_mag)
+    assert_close(x2.grad, gx_ref, gx_mag)

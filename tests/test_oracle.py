@@ -96,6 +96,43 @@ def test_ref_compat_matches_python_restatement(k):
         assert np.array_equal(pd, d[r]) and np.array_equal(pi, i[r]), r
 
 
+NAN_ROWS = os.path.join(os.path.dirname(__file__), "golden", "maxk_exact_nan.npz")
+
+
+def _torch_key(x):
+    """torch.topk's radix key (every NaN -> the largest key, all NaNs equal)."""
+    b = x.view(np.uint32).astype(np.uint64)
+    key = np.where(b & 0x80000000, ~b & 0xffffffff, b | 0x80000000)
+    return np.where((b & 0x7fffffff) > 0x7f800000, 0xffffffff, key)
+
+
+@pytest.mark.parametrize("k", [1, 8, 16, 32, 64])
+def test_exact_nan_order_matches_torch_topk(k):
+    """Exact mode ranks every NaN, either sign and any payload, above +Inf (torch.topk,
+    utils/models.py:15): the committed fixture equals the oracle bit for bit, and each row's
+    index set is torch.topk's wherever the k-th and (k+1)-th keys differ; where they tie (NaN
+    ties included), the selected keys are torch's and the tie goes to the lowest indices."""
+    with np.load(NAN_ROWS, allow_pickle=False) as z:
+        x, gd, gi = z["x"], z[f"data_k{k}"], z[f"index_k{k}"]
+    d, i = oracle.maxk(x, k, "exact")
+    assert np.array_equal(i, gi) and np.array_equal(d.view(np.uint32), gd.view(np.uint32))
+    ti = torch.topk(torch.from_numpy(x), k, dim=1).indices.numpy()
+    nan_rows = 0
+    for r in range(x.shape[0]):
+        key = _torch_key(x[r])
+        order = np.argsort(-key.astype(np.float64), kind="stable")   # ties: lowest index first
+        assert sorted(order[:k]) == list(gi[r]), r
+        assert np.array_equal(d[r].view(np.uint32), x[r][gi[r]].view(np.uint32)), r
+        # CPU torch.topk compares values, so +0 and -0 tie there (its GPU radix keys order them)
+        with np.errstate(invalid="ignore"):
+            ck = _torch_key(x[r] + np.float32(0.0))
+        assert sorted(ck[ti[r]]) == sorted(ck[gi[r]]), r                 # same keys as torch
+        if k < x.shape[1] and ck[order[k - 1]] != ck[order[k]]:
+            assert set(ti[r]) == set(gi[r]), r                         # no tie: same set
+        nan_rows += bool(np.isnan(x[r][gi[r]]).any())
+    assert nan_rows == x.shape[0]             # every row holds a NaN, so every row selects one
+
+
 EDGE = os.path.join(os.path.dirname(__file__), "golden", "maxk_refcompat_edge.npz")
 
 

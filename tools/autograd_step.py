@@ -3,7 +3,9 @@ graph, D = 256, k = 16 (or --k), x [N, D] requiring grad; one step = maxk_aggreg
 forward + backward with a given upstream gradient. Prints the step's device time (HIP events),
 the host time per step (wall clock of the Python calls without synchronising, i.e. how long
 the CPU takes to queue it), and the kernel times of its parts measured alone: top-k, SpGEMM,
-SSpMM, MaxK scatter.
+SSpMM, MaxK scatter. Round 6: also the unfused composition (MaxKFunction -> SpGEMMFunction,
+whose forward packs / scans the tables) in the same process, and the fused parts (top-k with
+statistics in the plan's layout, forward given the statistics).
 
   python tools/autograd_step.py [--dataset reddit] [--k 16]
 """
@@ -66,21 +68,40 @@ def main():
         y = mk.maxk_aggregate(x, graph, k)
         y.backward(g)
 
+    def step_unfused():  # round 5's composition: MaxKFunction -> SpGEMMFunction (the forward
+        x.grad = None    # packs / scans the CBSR tables it is handed)
+        sd, si = mk.maxk(x, k)
+        y = mk.spgemm(sd, si, graph, d)
+        y.backward(g)
+
     t_step = timeit(step)
     t_fresh = timeit(step_fresh)
+    t_unfused = timeit(step_unfused)
+    t_fresh2 = timeit(step_fresh)   # again, after the unfused variant (order effects)
     t_host = host_time(step_fresh)
     plan = graph.plan(d, k)
     sp_data, sp_index = mk.maxk_forward(x.detach(), k, return_index=True)
     out = torch.empty(n, d, device=dev)
     gsp = torch.empty(n, k, device=dev)
+    rd, ri = plan.new_cbsr()
+    st = mk.ops.topk_stats_buffer(dev)
+    mk.maxk_forward(x.detach(), k, return_index=True, out=(rd, ri), stats=st)
+    fused = {
+        "topk_stats_layout_ms": timeit(lambda: mk.maxk_forward(x.detach(), k, return_index=True,
+                                                                out=(rd, ri), stats=st)),
+        "spgemm_fwd_given_stats_ms": timeit(lambda: plan.forward(rd, ri, out,
+                                                                 stats=st[:2].view(1, 2))),
+    }
     parts = {
         "topk_ms": timeit(lambda: mk.maxk_forward(x.detach(), k, return_index=True)),
         "spgemm_fwd_ms": timeit(lambda: plan.forward(sp_data, sp_index, out)),
         "sspmm_bwd_ms": timeit(lambda: plan.backward(g, sp_index, gsp)),
         "maxk_scatter_ms": timeit(lambda: mk.maxk_backward(gsp, sp_index, d)),
     }
-    print(json.dumps({"dataset": args.dataset, "k": k, "step_ms": t_step, "step_ms_grad_none": t_fresh,
-                      "host_ms_per_step": t_host,
+    print(json.dumps({"dataset": args.dataset, "k": k, "fwd_layout": plan.info()["fwd_layout"],
+                      "step_ms": t_step, "step_ms_grad_none": t_fresh,
+                      "step_ms_grad_none_again": t_fresh2, "step_ms_unfused": t_unfused,
+                      "host_ms_per_step": t_host, "fused_parts": fused,
                       "parts": parts, "parts_sum_ms": sum(parts.values())}), flush=True)
 
 
