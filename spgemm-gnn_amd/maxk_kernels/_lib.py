@@ -27,8 +27,8 @@ SIGNATURES = {
     "maxk_topk_cbsr_count": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
     "maxk_topk_cbsr_tables": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32,
                                              _i32, _vp]),
-    "maxk_topk_cbsr_ex": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32,
-                                         _i32, _vp]),
+    "maxk_topk_cbsr_ex": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
+                                         _i32, _i32, _i32, _vp]),
     "maxk_scatter_backward": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "maxk_scatter_backward_tables": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
     "maxk_plan_create": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp,
@@ -71,8 +71,8 @@ SIGNATURES = {
 }
 
 
-# maxk_topk_cbsr_ex's stats buffer (uint32 words; the pair is words 0-1, the rest scratch)
-TOPK_STATS_WORDS = 8194
+# maxk_topk_cbsr_ex's statistics scratch (MAXK_TOPK_STATS_SCRATCH_BYTES)
+TOPK_STATS_SCRATCH_BYTES = 32768
 
 
 class PlanOptions(ctypes.Structure):

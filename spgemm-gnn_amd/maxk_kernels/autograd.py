@@ -268,10 +268,10 @@ class MaxKAggregateFunction(torch.autograd.Function):
         d = x.shape[1]
         plan = graph.plan(d, k)
         sp_data, sp_index = plan.new_cbsr()
-        stats = ops.topk_stats_buffer(x.device)
+        stats = torch.empty(2, dtype=torch.int32, device=x.device)
         res = ops.maxk_forward(x, k, mode=mode, return_index=True, out=(sp_data, sp_index),
                                stats=stats, return_count=mode != "exact")
-        out = plan.forward(sp_data, sp_index, stats=stats[:2].view(1, 2))
+        out = plan.forward(sp_data, sp_index, stats=stats.view(1, 2))
         ctx.save_for_backward(sp_index, *res[2:])
         ctx.plan = plan
         ctx.dim_origin = d

@@ -178,13 +178,32 @@ class ShardedAggregation:
         top-k here (``maxk_forward(h, k, out=...)``) and ``gather`` sends them as they are."""
         return self.send_data[: self.n_local], self.send_index[: self.n_local]
 
+    def local_topk(self, h_local: torch.Tensor, mode: str = "exact"):
+        """This rank's top-k written straight into its send records, with the fixed-point
+        statistics pair fused into the same launch (maxk_topk_cbsr_ex) and written into the
+        block's spare record: the NEXT exchange (one only, and only if no torch op has written
+        the records since) skips its statistics pass. Returns the ``(sp_data, sp_index)`` views
+        of :meth:`local_buffers`."""
+        from .ops import maxk_forward
+        sd, si = self.local_buffers()
+        maxk_forward(h_local, self.dim_k, mode=mode, return_index=True, out=(sd, si),
+                     stats=self._stats_words_send if self.stats else None)
+        self._stats_version = self.send_rec._version if self.stats else None
+        return sd, si
+
     def _stage(self, sp_data_local: torch.Tensor, sp_index_local: torch.Tensor) -> None:
         n = self.n_local
+        fresh = getattr(self, "_stats_version", None)
         if sp_data_local.data_ptr() != self.send_data.data_ptr():
             self.send_data[:n].copy_(sp_data_local)
+            fresh = None
         if sp_index_local.data_ptr() != self.send_index.data_ptr():
             self.send_index[:n].copy_(sp_index_local)
-        if self.stats:  # this rank's pair, all-gathered with its rows
+            fresh = None
+        # this rank's pair, all-gathered with its rows: from the local_topk just before (its
+        # records unchanged since: no torch op has bumped their version), else one pass
+        self._stats_version = None
+        if self.stats and fresh != self.send_rec._version:
             from .ops import cbsr_stats
             cbsr_stats(self.send_data[:n], self.send_index[:n], out=self._stats_words_send)
 

@@ -25,8 +25,8 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import (ACC_KINDS, BWD_ALGOS, COL_ORDERS, TOPK_STATS_WORDS, PlanInfo, PlanOptions,
-                   check, lib)
+from ._lib import (ACC_KINDS, BWD_ALGOS, COL_ORDERS, TOPK_STATS_SCRATCH_BYTES, PlanInfo,
+                   PlanOptions, check, lib)
 
 TOPK_MODES = {"exact": 0, "ref_compat": 1}
 
@@ -89,11 +89,11 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
     :class:`maxk_kernels.dist.ShardedAggregation`). ``return_count=True``
     appends the int32 ``[N]`` number of filled slots per row (``k`` in exact mode; in
     ref_compat mode the slots past it are the reference's ``(0.0f, 0)`` padding).
-    ``stats``: a contiguous int32 CUDA tensor of :func:`topk_stats_buffer`'s size whose first
-    two elements receive the fixed-point statistics of the emitted table with the top-k
-    (``maxk_topk_cbsr_ex``; the rest is the launch's scratch): the pair
-    :meth:`GraphPlan.forward` takes as ``stats=stats[:2].view(1, 2)`` instead of its own pass
-    over the table.
+    ``stats``: a contiguous int32 CUDA tensor of 2 elements (e.g. a view into a record) that
+    receives the fixed-point statistics of the emitted table with the top-k
+    (``maxk_topk_cbsr_ex``; its scratch comes from torch's caching allocator): the pair
+    :meth:`GraphPlan.forward` takes as ``stats=stats.view(1, 2)`` instead of its own pass over
+    the table.
     """
     _need(input.is_cuda, "input must be a CUDA tensor")
     _need(input.is_contiguous(), "input must be contiguous")
@@ -114,24 +114,21 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
         ds = _table(sp_data, "out[0]", torch.float32, n, k)
         is_ = _table(sp_index, "out[1]", torch.uint8, n, k)
     count = torch.empty(n, dtype=torch.int32, device=input.device) if return_count else None
+    scratch = None
     if stats is not None:
         _need(stats.is_cuda and stats.device == input.device and stats.is_contiguous() and
-              stats.dtype == torch.int32 and stats.numel() >= TOPK_STATS_WORDS,
-              f"stats must be a contiguous int32 CUDA tensor of {TOPK_STATS_WORDS} elements on "
-              f"the input's device (topk_stats_buffer)")
+              stats.dtype == torch.int32 and stats.numel() == 2,
+              "stats must be a contiguous int32 CUDA tensor of 2 elements on the input's device")
+        scratch = torch.empty(TOPK_STATS_SCRATCH_BYTES, dtype=torch.uint8, device=input.device)
     with _device(input.device):
         check(lib.maxk_topk_cbsr_ex(_p(input), _p(sp_data), ds, _p(sp_index), is_, _p(count),
-                                    _p(stats), n, d, k, TOPK_MODES[mode], _stream()),
-              "maxk_forward")
+                                    _p(stats), _p(scratch), TOPK_STATS_SCRATCH_BYTES if
+                                    scratch is not None else 0, n, d, k, TOPK_MODES[mode],
+                                    _stream()), "maxk_forward")
     res = (sp_data, sp_index) if return_index else (sp_data,)
     if return_count:
         res = res + (count,)
     return res if len(res) > 1 else res[0]
-
-
-def topk_stats_buffer(device) -> torch.Tensor:
-    """The ``stats=`` buffer of :func:`maxk_forward` (MAXK_TOPK_STATS_WORDS int32)."""
-    return torch.empty(TOPK_STATS_WORDS, dtype=torch.int32, device=device)
 
 
 def maxk_backward(grad_output: torch.Tensor, indices: torch.Tensor,

@@ -68,10 +68,15 @@ def test_emulated_shards_match_oracle(gpu, world, opts, k):
         assert shard.stats
         a, b = part.rows(q)
         bd, bi = shard.local_buffers()
-        mk.maxk_forward(graphs.features(n, d, seed=15)[a:b].contiguous().to(gpu), k,
-                        out=(bd, bi))                       # top-k into the send records
+        h_q = graphs.features(n, d, seed=15)[a:b].contiguous().to(gpu)
+        mk.maxk_forward(h_q, k, out=(bd, bi))               # top-k into the send records
         assert torch.equal(bd, sd[a:b]) and torch.equal(bi, si[a:b])
         shard._stage(bd, bi)
+        pair = shard.send_rec[part.max_rows, :8].clone()    # cbsr_stats over the records
+        bd2, bi2 = shard.local_topk(h_q)                    # statistics fused into the top-k
+        assert torch.equal(bd2, sd[a:b]) and torch.equal(bi2, si[a:b])
+        assert torch.equal(shard.send_rec[part.max_rows, :8], pair)
+        shard._stage(bd2, bi2)                              # consumes the fused pair
         _fill_tables(part, sd, si, shard, gpu)
         # the rank's own statistics pair went out with its send records
         assert torch.equal(shard.send_rec[part.max_rows, :8],

@@ -321,3 +321,41 @@ def test_cbsr_stats_repeat_detection(gpu, k):
         got = float(np.uint32(st.cpu().numpy().view(np.uint32)[0, 0]).view(np.float32))
         want = xs.sum() * (1 + 2.0 ** -10) if rep else xs.max()
         assert abs(got - want) <= 1e-6 * want, (k, s, x, got, want)
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_skewed_column_blocks_keep_their_chunks(gpu, k):
+    """the chunk-count search may go below the nominal chunk count only while the
+    column blocks hold similar edge counts. A graph whose in-edges pile onto the first columns
+    (power-law source degrees, Zipf-like) has one block many times the mean: the plan keeps at
+    least the nominal task count (one round of CUs or more, every block cut into the same
+    number of chunks) and the backward matches the oracle."""
+    n, e = 120_000, 4_000_000
+    rs = np.random.RandomState(5)
+    deg = np.minimum(rs.lognormal(np.log(e / n) - 0.5, 1.0, n).astype(np.int64) + 1, n)
+    scale = e / deg.sum()
+    deg = np.maximum(1, (deg * scale).astype(np.int64))
+    ptr = np.zeros(n + 1, np.int64)
+    ptr[1:] = np.cumsum(deg)
+    cols = np.minimum((rs.pareto(0.7, int(ptr[-1])) * 50).astype(np.int64), n - 1)
+    idx = np.concatenate([np.sort(cols[ptr[r]:ptr[r + 1]]) for r in range(n)]).astype(np.int32)
+    ptr = ptr.astype(np.int32)
+    val = rs.uniform(0.1, 1.0, idx.size).astype(np.float32)
+    dptr, didx, dval = (torch.from_numpy(a).to(gpu) for a in (ptr, idx, val))
+    plan = mk.GraphPlan(dptr, didx, dval, n, idx.size, 256, k, options={"bwd_algo": 1})
+    info = plan.info()
+    counts = np.bincount(idx, minlength=n)
+    cb = info["bwd_block_cols"]
+    per_block = np.add.reduceat(counts, np.arange(0, n, cb))
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    print(f"k={k}: {info['bwd_blocks']} blocks, largest {per_block.max()} edges vs mean "
+          f"{per_block.mean():.0f}; {info['bwd_tasks']} tasks on {cus} CUs")
+    assert per_block.max() > 2 * per_block.mean()           # the case the bound is for
+    assert info["bwd_tasks"] >= min(cus, info["bwd_blocks"])
+    x = graphs.features(n, 256, seed=k)
+    _, oi = oracle.maxk(x.numpy(), k)
+    g = graphs.features(n, 256, seed=k + 1)
+    gs = plan.backward(g.to(gpu), torch.from_numpy(oi).to(gpu))
+    ref, mag = oracle.sspmm_backward(ptr, idx, val, g.numpy(), oi, with_mag=True)
+    ok, worst = oracle.close_enough(gs.cpu().numpy(), ref, mag)
+    assert ok, worst

@@ -953,10 +953,10 @@ def test_topk_fused_stats_equal_cbsr_stats(gpu, k, mode, records):
         else:
             sd = torch.empty((n, k), device=gpu)
             si = torch.empty((n, k), dtype=torch.uint8, device=gpu)
-        st = mk.ops.topk_stats_buffer(gpu).fill_(-1)
+        st = torch.empty(2, dtype=torch.int32, device=gpu).fill_(-1)
         mk.maxk_forward(xd, k, mode=mode, return_index=True, out=(sd, si), stats=st)
         ref = mk.cbsr_stats(sd, si)
-        assert st[:2].tolist() == ref.view(-1).tolist(), (r, st[:2].tolist(), ref.tolist())
+        assert st.tolist() == ref.view(-1).tolist(), (r, st.tolist(), ref.tolist())
         d0, i0 = mk.maxk_forward(xd, k, mode=mode, return_index=True)
         assert torch.equal(si.cpu(), i0.cpu())
         assert np.array_equal(sd.cpu().numpy().view(np.uint32), d0.cpu().numpy().view(np.uint32))
@@ -964,16 +964,17 @@ def test_topk_fused_stats_equal_cbsr_stats(gpu, k, mode, records):
 
 def test_topk_fused_stats_empty_and_tiny(gpu):
     """N = 0 writes the all-zero pair (the forward then takes f64); N = 1 and N = 5."""
-    st = mk.ops.topk_stats_buffer(gpu).fill_(7)
+    st = torch.empty(2, dtype=torch.int32, device=gpu).fill_(7)
     x = torch.empty((0, 64), device=gpu)
     mk.maxk_forward(x, 8, return_index=True, stats=st)
-    assert st[:2].tolist() == [0, 0]
+    assert st.tolist() == [0, 0]
     for n in (1, 5):
         x = graphs.features(n, 64, seed=n).to(gpu)
         sd, si = mk.maxk_forward(x, 8, return_index=True, stats=st)
-        assert st[:2].tolist() == mk.cbsr_stats(sd, si).view(-1).tolist()
+        assert st.tolist() == mk.cbsr_stats(sd, si).view(-1).tolist()
     with pytest.raises(RuntimeError, match="stats must be"):
-        mk.maxk_forward(x, 8, return_index=True, stats=st[:2])
+        mk.maxk_forward(x, 8, return_index=True, stats=torch.empty(3, dtype=torch.int32,
+                                                                   device=gpu))
 
 
 @pytest.mark.parametrize("k", [8, 16, 24, 32, 64])

@@ -21,7 +21,7 @@ for name in ("reddit", "ogbn-products"):
     n, _ = graphs.DATASETS[name]
     h = graphs.features(n, 256, seed=97, device=dev)
     for k in (8, 16, 32, 64):
-        st = mk.ops.topk_stats_buffer(dev)
+        st = torch.empty(2, dtype=torch.int32, device=dev)
         for mode, stats in (("exact", None), ("exact", st), ("ref_compat", None),
                             ("ref_compat", st)):
             fn = lambda: mk.maxk_forward(h, k, mode=mode, return_index=True, stats=stats)  # noqa: E731
