@@ -25,6 +25,8 @@
 #include <cstring>
 #include <vector>
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace maxk {
@@ -341,6 +343,25 @@ __global__ void iota_kernel(int n, int32_t* __restrict__ out) {
 }
 
 static void dfree(void* q) { if (q) (void)hipFree(q); }
+
+// The large streamed plan arrays (forward edge words, backward records). MAXK_PLAN_MALLOC=
+// contiguous asks the runtime for physically contiguous memory (hipDeviceMallocContiguous),
+// falling back to hipMalloc when it cannot (round 6 experiment on allocation-dependent kernel
+// times).
+static hipError_t plan_malloc(void** q, size_t bytes) {
+  static const int mode = [] {
+    const char* e = std::getenv("MAXK_PLAN_MALLOC");
+    return (e && std::string(e) == "contiguous") ? 1 : 0;
+  }();
+  if (mode == 1 && hipExtMallocWithFlags(q, bytes, hipDeviceMallocContiguous) == hipSuccess)
+    return hipSuccess;
+  (void)hipGetLastError();
+  return hipMalloc(q, bytes);
+}
+template <class T>
+static hipError_t plan_malloc(T** q, size_t bytes) {
+  return plan_malloc(reinterpret_cast<void**>(q), bytes);
+}
 
 static int grid_for(int64_t n, int threads) {
   int64_t g = (n + threads - 1) / threads;
@@ -836,7 +857,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
         if (e == hipSuccess)
           e = hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_kin, d_kout, d_ids, p->fwd_perm,
                                                  (int)E, 0, cbits + tbits, s);
-        if (e == hipSuccess) e = hipMalloc(&p->fwd_cv, sizeof(uint2) * E);
+        if (e == hipSuccess) e = plan_malloc(&p->fwd_cv, sizeof(uint2) * E);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->fwd_perm,
                            idx, d_rl, val, E, p->fwd_cv, true);
@@ -1082,7 +1103,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     }
     if (!twopass) p->bwd_row_order = row_hash ? 2 : 1;
     if (twopass) {
-      PLAN_TRY(hipMalloc(&p->bwd_erec, sizeof(uint32_t) * 2 * (size_t)E));
+      PLAN_TRY(plan_malloc(&p->bwd_erec, sizeof(uint32_t) * 2 * (size_t)E));
       // row chunks: the workspace holds one chunk's products
       int P = o.bwd_tp_chunks > 0
                   ? o.bwd_tp_chunks
@@ -1384,7 +1405,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   }
   if (!twopass && E > 0) {
     // the column blocks' records (padded: a wave may read past the last task's end)
-    PLAN_TRY(hipMalloc(&p->bwd_rec, sizeof(uint32_t) * 3 * (size_t)(E + kBwdRecPad)));
+    PLAN_TRY(plan_malloc(&p->bwd_rec, sizeof(uint32_t) * 3 * (size_t)(E + kBwdRecPad)));
     PLAN_TRY(hipMemsetAsync(p->bwd_rec + 3 * E, 0, sizeof(uint32_t) * 3 * kBwdRecPad, s));
     hipLaunchKernelGGL(build_bwd_rec_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->bwd_perm,
                        brow, bcol, val, E, C, D, p->bwd_big, p->bwd_rec);

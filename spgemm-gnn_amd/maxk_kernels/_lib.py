@@ -29,6 +29,7 @@ SIGNATURES = {
                                              _i32, _vp]),
     "maxk_topk_cbsr_ex": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
                                          _i32, _i32, _i32, _vp]),
+    "maxk_topk_stats_scratch_bytes": (ctypes.c_int64, [_i32]),
     "maxk_scatter_backward": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _vp]),
     "maxk_scatter_backward_tables": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
     "maxk_plan_create": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp,
@@ -69,10 +70,6 @@ SIGNATURES = {
     "maxk_dense_spmm_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),
     "maxk_warp4_build": (ctypes.c_int, [_vp, _i32, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
 }
-
-
-# maxk_topk_cbsr_ex's statistics scratch (MAXK_TOPK_STATS_SCRATCH_BYTES)
-TOPK_STATS_SCRATCH_BYTES = 32768
 
 
 class PlanOptions(ctypes.Structure):

@@ -25,8 +25,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import (ACC_KINDS, BWD_ALGOS, COL_ORDERS, TOPK_STATS_SCRATCH_BYTES, PlanInfo,
-                   PlanOptions, check, lib)
+from ._lib import ACC_KINDS, BWD_ALGOS, COL_ORDERS, PlanInfo, PlanOptions, check, lib
 
 TOPK_MODES = {"exact": 0, "ref_compat": 1}
 
@@ -114,16 +113,16 @@ def maxk_forward(input: torch.Tensor, k: int, mode: str = "exact",
         ds = _table(sp_data, "out[0]", torch.float32, n, k)
         is_ = _table(sp_index, "out[1]", torch.uint8, n, k)
     count = torch.empty(n, dtype=torch.int32, device=input.device) if return_count else None
-    scratch = None
+    scratch, sbytes = None, 0
     if stats is not None:
         _need(stats.is_cuda and stats.device == input.device and stats.is_contiguous() and
               stats.dtype == torch.int32 and stats.numel() == 2,
               "stats must be a contiguous int32 CUDA tensor of 2 elements on the input's device")
-        scratch = torch.empty(TOPK_STATS_SCRATCH_BYTES, dtype=torch.uint8, device=input.device)
+        sbytes = int(lib.maxk_topk_stats_scratch_bytes(n))
+        scratch = torch.empty(sbytes, dtype=torch.uint8, device=input.device)
     with _device(input.device):
         check(lib.maxk_topk_cbsr_ex(_p(input), _p(sp_data), ds, _p(sp_index), is_, _p(count),
-                                    _p(stats), _p(scratch), TOPK_STATS_SCRATCH_BYTES if
-                                    scratch is not None else 0, n, d, k, TOPK_MODES[mode],
+                                    _p(stats), _p(scratch), sbytes, n, d, k, TOPK_MODES[mode],
                                     _stream()), "maxk_forward")
     res = (sp_data, sp_index) if return_index else (sp_data,)
     if return_count:

@@ -9,8 +9,10 @@ offset 0), and timed (HIP events, median of 3 rounds of 20):
   gout  the rank's grad_out rows [n_local, D] f32 (gathered)
   sel   the gathered record table (selectors at the record stride)
 
-Then P fresh plans (new hipMallocs inside the plan) with all buffers at offset 0. Every line
-carries the buffers' virtual addresses and their offsets within a 2 MiB fragment.
+Then the shard's plan (plan 0) and P fresh plans (new hipMallocs inside each plan), all per-call
+buffers at offset 0, each timed twice in turn. Offset lines carry the buffers' virtual
+addresses and their offsets within a 2 MiB fragment. MAXK_PLAN_MALLOC=contiguous makes the
+plans allocate their streamed arrays physically contiguous (plan.hip plan_malloc).
 
   python tools/shard_alloc.py [--rank 3] [--world 8] [--k 16] [--offsets 0,4096,...]
                               [--plans 8] [--only out:0,out:1048576]
@@ -60,6 +62,13 @@ def main():
     ap.add_argument("--only", default="", help="buf:off,... : time just these placements "
                     "(for PMC passes); plans are skipped")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--cross", default="",
+                    help="buf: time every plan (shard's + --plans fresh) at every --offsets "
+                         "placement of that buffer, twice (a plan x offset matrix; out or ws "
+                         "only: the placements of one arena overlap)")
+    ap.add_argument("--plans-only", action="store_true",
+                    help="skip the offset sweep: the shard's plan and --plans fresh plans, each "
+                         "timed twice (MAXK_PLAN_MALLOC selects their allocation)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, e = graphs.DATASETS["reddit"]
@@ -128,7 +137,18 @@ def main():
             ms = timeit(lambda: launch(plan, *v), reps=args.reps)
             print(json.dumps({"rank": q, "buf": nm, "off": int(off), "bwd_ms": ms}), flush=True)
         return
-    for nm in ("out", "ws", "gout", "sel"):
+    if args.cross:
+        plans = [plan] + [mk.GraphPlan(pr, ix, vl, nloc, plan.num_edges, d, k, num_cols=ncol)
+                          for _ in range(args.plans)]
+        offs = [int(x) for x in args.offsets.split(",")]
+        views_at = {off: setup(dict(zero, **{args.cross: off})) for off in offs}
+        for rnd in range(2):
+            for i, p2 in enumerate(plans):
+                row = [timeit(lambda: launch(p2, *views_at[off]), reps=args.reps) for off in offs]
+                print(json.dumps({"rank": q, "buf": args.cross, "plan": i, "round": rnd,
+                                  "offsets": offs, "bwd_ms": row}), flush=True)
+        return
+    for nm in (() if args.plans_only else ("out", "ws", "gout", "sel")):
         for off in [int(x) for x in args.offsets.split(",")]:
             place = dict(zero, **{nm: off})
             v = setup(place)
@@ -137,13 +157,15 @@ def main():
             print(json.dumps({"rank": q, "buf": nm, "off": off, "bwd_ms": ms,
                               "max_abs_diff_vs_offset0": diff, "addr": addrs(*v)}), flush=True)
     # fresh plans (their internal buffers at new addresses), per-call buffers at offset 0
-    keep = []
+    keep = [plan]
     for i in range(args.plans):
-        p2 = mk.GraphPlan(pr, ix, vl, nloc, plan.num_edges, d, k, num_cols=ncol)
-        keep.append(p2)
-        ms = timeit(lambda: launch(p2, *ref), reps=args.reps)
-        print(json.dumps({"rank": q, "plan": i, "bwd_ms": ms,
-                          "plan_device_bytes": p2.device_bytes}), flush=True)
+        keep.append(mk.GraphPlan(pr, ix, vl, nloc, plan.num_edges, d, k, num_cols=ncol))
+    malloc = os.environ.get("MAXK_PLAN_MALLOC", "default")
+    for rnd in range(2):
+        for i, p2 in enumerate(keep):
+            ms = timeit(lambda: launch(p2, *ref), reps=args.reps)
+            print(json.dumps({"rank": q, "plan": i, "round": rnd, "bwd_ms": ms, "malloc": malloc,
+                              "plan_device_bytes": p2.device_bytes}), flush=True)
 
 
 if __name__ == "__main__":
