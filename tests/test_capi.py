@@ -295,3 +295,40 @@ def test_create_ex_reads_only_the_round1_layout():
                                     ctypes.byref(h))
     assert rc == -1 and "external_workspace" in lib.maxk_last_error().decode()
     assert not h.value
+
+
+def test_backward_shapes_without_a_kernel_refused_on_host():
+    """ABI 4: an explicit bwd_unroll that the explicit bwd_waves has no kernel for
+    (16 waves run 8 sub-steps only; 12 waves 8 or 12) is refused with MAXK_ERR_INVALID_ARG
+    before any device call, instead of being replaced by 8; the combinations that exist pass
+    the option checks (and then fail on the null graph)."""
+    lib = _lib.lib
+    h = ctypes.c_void_p(0)
+    for waves, unroll, ok in ((16, 12, False), (16, 16, False), (12, 16, False), (16, 8, True),
+                              (12, 12, True), (12, 8, True), (8, 16, True), (8, 12, True),
+                              (0, 16, True), (0, 12, True)):
+        opts = _lib.PlanOptions()
+        opts.bwd_waves, opts.bwd_unroll = waves, unroll
+        rc = lib.maxk_plan_create_sized(None, None, None, 10, 10, 100, 256, 16, ctypes.byref(opts),
+                                        ctypes.sizeof(opts), None, None, ctypes.byref(h))
+        msg = lib.maxk_last_error().decode()
+        assert rc == -1, (waves, unroll)
+        assert ("bwd_waves" in msg) != ok, (waves, unroll, msg)
+    assert not h.value
+
+
+def test_topk_stats_scratch_contract():
+    """maxk_topk_cbsr_ex with stats needs maxk_topk_stats_scratch_bytes(N) of scratch: one
+    8-B partial pair per 4 rows (per wave of the exact kernel, per work-group of the
+    ref_compat one), refused on the host when smaller or missing."""
+    lib = _lib.lib
+    assert lib.maxk_topk_stats_scratch_bytes(0) == 64
+    assert lib.maxk_topk_stats_scratch_bytes(16) == 8 * 4 + 64
+    assert lib.maxk_topk_stats_scratch_bytes(17) == 8 * 8 + 64
+    P = ctypes.c_void_p
+    n = 100
+    need = lib.maxk_topk_stats_scratch_bytes(n)
+    for scratch, nbytes in ((None, need), (P(16), need - 1)):
+        rc = lib.maxk_topk_cbsr_ex(P(16), P(16), 0, P(16), 0, None, P(16), scratch, nbytes, n,
+                                   256, 16, 0, None)
+        assert rc == -1 and "scratch" in lib.maxk_last_error().decode()

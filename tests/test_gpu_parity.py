@@ -617,7 +617,7 @@ def test_dense_spmm_vs_oracle(gpu):
 PLAN_OPTIONS = [
     dict(fwd_tile_rows=16), dict(fwd_tile_rows=1), dict(fwd_tile_rows=64), dict(fwd_task_cap=512),
     dict(fwd_rotate=2), dict(fwd_rot_windows=64), dict(fwd_rot_windows=3, fwd_rot_rate=1),
-    dict(bwd_unroll=12), dict(bwd_unroll=16), dict(bwd_waves=12), dict(bwd_waves=12, bwd_unroll=16), dict(bwd_waves=12, bwd_unroll=12),
+    dict(bwd_unroll=12), dict(bwd_unroll=16), dict(bwd_waves=12), dict(bwd_waves=8, bwd_unroll=16), dict(bwd_waves=12, bwd_unroll=12),
     dict(bwd_waves=16), dict(bwd_waves=16, bwd_features_per_lane=2),
     dict(bwd_waves=16, bwd_piece_edges=500, bwd_slot_groups=2),
     # window hand-out: static interleave or an LDS counter, forward and backward
