@@ -1017,3 +1017,49 @@ def test_maxk_aggregate_fused_equals_unfused(gpu, k, mode):
     gx_mag[rows[filled], oi[filled]] = gmag[filled]
     assert_close(x1.grad, gx_ref, gx_mag)
     assert_close(x2.grad, gx_ref, gx_mag)
+
+
+# ------------------------------------------------ the reference's own layer code, unchanged
+def test_reference_layer_call_sequences(gpu):
+    """With this package first on PYTHONPATH, the reference's unchanged training script
+    (maxk_gnn_integrated.py:21 -> utils/integrated_models.py:6 -> utils/maxk_layers.py:10
+    `import maxk_kernels`) calls these functions exactly as below, with the argument types that
+    code builds (replayed here; the reference itself, which needs DGL, is not imported):
+
+    * maxk_layers.py:21   maxk_forward(input, k) -> [N, k] f32 values;
+    * maxk_layers.py:23,40 maxk_backward(grad [N, k], torch.topk(input, k)[1] int64, unsorted)
+      -> [N, max(index) + 1];
+    * maxk_layers.py:166-171 (SAGE) spgemm_forward(ptr.int(), idx.int(), f32 weights from a
+      Python list, torch.stack of f32 rows, torch.stack of u8 rows, N, E, maxk, out_feats)
+      -> (out, sp_index), out against the oracle;
+    * maxk_layers.py:380-385 (GCN) spgemm_forward with DGL's int64 adj_tensors: refused with
+      the reference binding's message (bindings.cpp:45-54 checks int32), as there."""
+    p, ix, v = GRAPHS["synthetic"]()
+    n, d, k = p.size - 1, 64, 16
+    x = graphs.features(n, d, seed=71).to(gpu)
+    out = mk.maxk_forward(x, k)                                    # :21
+    assert out.shape == (n, k) and out.dtype == torch.float32
+    od, oi = oracle.maxk(x.cpu().numpy(), k)
+    assert np.array_equal(out.cpu().numpy(), od)
+    indices = torch.topk(x, k, dim=1)[1]                           # :23, int64, value order
+    g = torch.randn(n, k, device=gpu)
+    gi = mk.maxk_backward(g, indices)                              # :40
+    width = int(indices.max()) + 1
+    ref = np.zeros((n, width), np.float32)
+    ind = indices.cpu().numpy()
+    for j in range(k):                                             # last slot wins
+        ref[np.arange(n), ind[:, j]] = g.cpu().numpy()[:, j]
+    assert gi.shape == (n, width) and np.array_equal(gi.cpu().numpy(), ref)
+    # SAGE aggregation as _aggregate_with_custom_kernel builds its arguments
+    ptr, idx = torch.from_numpy(p).long().to(gpu), torch.from_numpy(ix).long().to(gpu)
+    deg = np.diff(p)
+    w = torch.tensor([1.0 / max(int(c), 1) for c in deg for _ in range(int(c))], device=gpu)
+    sp_data = torch.stack([out[i] for i in range(n)])              # :233-262, contiguous
+    sp_index = torch.stack([torch.from_numpy(oi[i]).to(gpu) for i in range(n)])
+    agg, si = mk.spgemm_forward(ptr.int(), idx.int(), w, sp_data, sp_index, n, ix.size, k, d)
+    assert si is sp_index
+    yref, ymag = oracle.spgemm_forward(p, ix, w.cpu().numpy(), od, oi, d, with_mag=True)
+    assert_close(agg, yref, ymag)
+    # GCN: DGL's adj_tensors('csr') are int64; the reference binding requires int32
+    with pytest.raises(RuntimeError, match="ptr must be int32"):
+        mk.spgemm_forward(ptr, idx, w, sp_data, sp_index, n, ix.size, k, d)
