@@ -27,6 +27,7 @@ constexpr int kMaxDim = 256;            // u8 selectors => D <= 256
 constexpr int kFwdUnroll = 8;           // independent sub-steps in flight per wave
 constexpr int kFwdFlagChunk3 = 1;       // forward kernel flags (template FL): lane-chunk records
 constexpr int kFwdFlagQuad = 2;         // quad-shared edge-word loads
+constexpr int kFwdFlagChunk2 = 4;       // pair-chunk records: 2 values + their selectors per 16 B
 constexpr int kBwdTasksPerCu = 2;
 constexpr int kBwdMinTaskEdges = 100000;  // a chunk's flush (C*k stores) vs its edges
 constexpr int kXcds = 8;
@@ -173,6 +174,7 @@ struct maxk_plan {
   int32_t fwd_phases = 1;        // column windows of the rotated sweep (1: no rotation)
   int32_t fwd_rot_ticks = 0;     // > 0: rotated sweeps, s_memrealtime ticks per window
   int32_t fwd_chunk3 = 0;        // lane-chunk records: 3 values + their selectors per 16 B
+  int32_t fwd_chunk2 = 0;        // pair-chunk records: 2 values + their selectors per 16 B
   int32_t fwd_quad = 0;          // quad-shared edge-word loads
   int32_t fwd_two_tables = 0;    // gather from sp_data / sp_index directly (no pack)
   int32_t* fwd_phase_off = nullptr;  // [tasks][phases + 1] edge offsets per window

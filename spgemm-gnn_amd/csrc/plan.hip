@@ -582,8 +582,8 @@ static int check_options(const maxk_plan_options& o) {
                      "fwd_prefetch / bwd_prefetch = 1");
   MAXK_CHECK_REMOVED(o.fwd_record_bytes == 0, "fwd_record_bytes");
   MAXK_CHECK_REMOVED(o.fwd_branchless == 0 || o.fwd_branchless == 1, "fwd_branchless = 2");
-  MAXK_CHECK_ARG(o.fwd_chunk3 >= 0 && o.fwd_chunk3 <= 2,
-                 "maxk_plan_create: fwd_chunk3 must be 0, 1 or 2");
+  MAXK_CHECK_ARG(o.fwd_chunk3 >= 0 && o.fwd_chunk3 <= 3,
+                 "maxk_plan_create: fwd_chunk3 must be 0, 1, 2 or 3");
   MAXK_CHECK_REMOVED(o.bwd_cas64 == 0 || o.bwd_cas64 == 1, "bwd_cas64 = 2");
   MAXK_CHECK_REMOVED(o.quad_loads == 0, "quad_loads");
   MAXK_CHECK_ARG(o.fwd_two_tables >= 0 && o.fwd_two_tables <= 2,
@@ -656,12 +656,25 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   // where the 4-wave sweep's column span is what keeps the records in L2: k = 16 (8 waves
   // +36 %, L2 hit 62 -> 37 %) and k = 48 (+28 %; 4 sub-steps per wave instead, -4 %).
   // profiles/r05/fwd_waves_sweep.jsonl
-  p->fwd_waves = o.fwd_waves ? o.fwd_waves : (k == 16 && o.fwd_unroll != 4 ? 4 : 8);
+  const int waves_rec = o.fwd_waves ? o.fwd_waves : (k == 16 && o.fwd_unroll != 4 ? 4 : 8);
+  // pair chunks {2 values, 2 selector bytes} per lane (round 6): one gather gives a lane its
+  // values and selectors, k / 2 lanes per edge (quad-shared edge words when k / 2 % 4 == 0).
+  // Half the edges per instruction of the records kernel, so 8 waves keep as many in flight
+  // (Reddit k = 16: 4 waves 1.419 ms, 8 waves 1.029 against 1.078 for the records kernel).
+  // Default at k = 16, pack fused into the statistics pass (profiles/r06/fwd_pair_chunks.jsonl,
+  // forward with its pass: Reddit 1.077 -> 1.008 ms, ogbn-proteins 0.712 -> 0.666, ogbn-products
+  // 3.02 -> 2.92, yelp 0.521 -> 0.468, flickr 0.080 -> 0.067); not at k = 8 (4 lanes: 0.896
+  // vs 0.891 lane chunks), 12 / 20 / 24 (6 / 10 / 12 lanes, no quads: +13..+92 %) or 32 (+19 %)
+  p->fwd_chunk2 = (o.fwd_chunk3 == 3 || (o.fwd_chunk3 == 0 && k == 16)) && k % 2 == 0 &&
+                  k / 2 <= kWave;
+  p->fwd_waves = p->fwd_chunk2 && !o.fwd_waves ? 8 : waves_rec;
   p->fwd_unroll = o.fwd_unroll ? o.fwd_unroll : (p->fwd_waves == 8 && k == 48 ? 4 : 8);
   // lane-chunk records by default where the 4-values-per-lane layout fits k badly (Reddit:
   // k = 8 0.95 vs 1.02 ms, k = 24 1.93 vs 2.09 ms; k = 16 / 32 / 64 are slower with chunks),
   // and for every k % 4 != 0 up to 192 (beyond: one lane per feature, f64)
-  p->fwd_chunk3 = (o.fwd_chunk3 == 1 || (o.fwd_chunk3 == 0 && k % 16 != 0)) && (k + 2) / 3 <= kWave;
+  p->fwd_chunk3 = (o.fwd_chunk3 == 1 ||
+                   ((o.fwd_chunk3 == 0 || (o.fwd_chunk3 == 3 && !p->fwd_chunk2)) && k % 16 != 0)) &&
+                  (k + 2) / 3 <= kWave;
   // Fixed-point forward (LdsFix; the packed 4-values-per-lane and lane-chunk kernels).
   // Measured (tools/fwd_fixed_sweep.py, fixed vs f64 ms): Reddit k = 16 1.22 / 1.34,
   // k = 24 1.57 / 1.95, k = 32 1.80 / 2.46, k = 64 3.45 / 4.81; ogbn-proteins k = 16 0.80 / 0.93,
@@ -671,7 +684,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   const bool big_table = (double)std::max(NC, 1) * 5.0 * k >
                          (k >= 32 ? kFwdPackedTableBytes : kFwdPackedTableBytes16);
   p->fwd_fixed = (o.fwd_fixed == 1 || (o.fwd_fixed == 0 && k >= 16 && !big_table)) &&
-                 (k % 4 == 0 || p->fwd_chunk3);
+                 (k % 4 == 0 || p->fwd_chunk3 || p->fwd_chunk2);
   // forward quad-shared edge-word loads with the fixed-point kernel (k = 16 1.19 -> 1.16 ms,
   // k = 32 1.81 -> 1.78); neutral-to-slower on the f64 kernel
   p->fwd_quad = p->fwd_fixed;
@@ -892,7 +905,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
     // the whole pass and the aligned sweep finds little to share (ogbn-products, 50 edges per
     // column, k = 32: 4.79 -> 4.71 ms without it; Reddit, 493: k = 16 1.11 -> 1.08 with it)
     const bool low_reuse = o.fwd_rotate == 0 && NC > 0 && (double)E / NC < 64.0;
-    if (o.fwd_rotate != 2 && !low_reuse && (k % 4 == 0 || p->fwd_chunk3)) {
+    if (o.fwd_rotate != 2 && !low_reuse && (k % 4 == 0 || p->fwd_chunk3 || p->fwd_chunk2)) {
       // the fixed-point kernel sweeps faster: more windows at large k, a higher slot rate
       // (tools/fwd_opts_sweep.py, Reddit: k = 16 1.23 -> 1.19 ms with 260 M edges/s per slot,
       // k = 32 1.81 -> 1.77 with 140 M and 32 windows, k = 64 3.44 -> 3.23 with 64 windows)
@@ -936,14 +949,14 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   const bool sel_l2 = (double)std::max(NC, 1) * k <= kFwdSelL2Bytes;
   const bool few_edges = E < kFwdPackMinEdgesPerCol * std::max(NC, 1) ||
                          (sel_l2 && E < kFwdPackMinEdgesPerColL2 * std::max(NC, 1));
-  p->fwd_two_tables = !p->fwd_chunk3 && k % 4 == 0 &&
+  p->fwd_two_tables = !p->fwd_chunk3 && !p->fwd_chunk2 && k % 4 == 0 &&
                       (o.fwd_two_tables == 1 ||
                        (o.fwd_two_tables == 0 &&
                         (k >= 64 || (!big_table && (k >= 32 || few_edges)))));
   if (p->fwd_two_tables) {
     // no workspace: the kernel gathers from sp_data / sp_index
-  } else if (p->fwd_chunk3 && NC > 0) {
-    const int b = (k + 2) / 3 * 16;
+  } else if ((p->fwd_chunk3 || p->fwd_chunk2) && NC > 0) {
+    const int b = (p->fwd_chunk3 ? (k + 2) / 3 : k / 2) * 16;
     p->fwd_rec_bytes = b <= 64 ? 64 : b <= 128 ? 128 : b;
     p->fwd_ws_bytes = (int64_t)NC * p->fwd_rec_bytes;
   } else if (k % 4 == 0 && NC > 0) {
@@ -1494,7 +1507,10 @@ extern "C" int maxk_plan_get_info_sized(const maxk_plan* p, maxk_plan_info* out,
   info.fwd_unroll = p->fwd_unroll;
   info.bwd_waves = p->bwd_twopass ? 0 : p->bwd_waves;  // the two-pass kernels have one shape
   info.bwd_unroll = p->bwd_twopass ? 0 : p->bwd_unroll;
-  if (p->fwd_chunk3) {
+  if (p->fwd_chunk2) {
+    info.fwd_layout = 4;
+    info.fwd_record_bytes = p->fwd_rec_bytes;
+  } else if (p->fwd_chunk3) {
     info.fwd_layout = 2;
     info.fwd_record_bytes = p->fwd_rec_bytes;
   } else if (p->dim_k % 4 != 0) {

@@ -126,11 +126,13 @@ __device__ __forceinline__ double fwd_fix_scale(int2 fix, const uint32_t* xs, in
 // (or its own nonzero selectors do not ascend): the same bound as the thread-per-row kernel
 // below, with the row sum added in another order (its 2^-10 headroom covers that).
 //
-// PACK: the same pass also writes the forward's packed CBSR records (k values, then the k
+// PACK 1: the same pass also writes the forward's packed CBSR records (k values, then the k
 // selector bytes, rec_bytes per row), so the per-call pack and the statistics cost one read
-// of the tables. STATS = false: the pack alone. The forward's split rows (summed atomically
-// by their segments) are zeroed here too, one launch before the forward.
-template <bool PACK, bool STATS>
+// of the tables; PACK 2: the pair-chunk records instead (plan->fwd_chunk2: lane q writes the
+// 16-B chunks 2q and 2q + 1, {2 values, their 2 selector bytes, 0}). STATS = false: the pack
+// alone. The forward's split rows (summed atomically by their segments) are zeroed here too,
+// one launch before the forward.
+template <int PACK, bool STATS>
 __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restrict__ x,
                                                           const uint8_t* __restrict__ sel,
                                                           int64_t nrows, int k, uint32_t* st0,
@@ -158,10 +160,14 @@ __global__ __launch_bounds__(256) void cbsr_stats4_kernel(const float* __restric
     if (live) {
       v = *reinterpret_cast<const float4*>(x + r * ds + 4 * q);
       s = *reinterpret_cast<const uint32_t*>(sel + r * is + 4 * q);
-      if constexpr (PACK) {
+      if constexpr (PACK == 1) {
         uint8_t* rp = rec + r * rec_bytes;
         *reinterpret_cast<float4*>(rp + 16 * q) = v;
         *reinterpret_cast<uint32_t*>(rp + 4 * k + 4 * q) = s;
+      } else if constexpr (PACK == 2) {
+        uint4* rp = reinterpret_cast<uint4*>(rec + r * rec_bytes) + 2 * q;
+        rp[0] = make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), s & 0xffffu, 0u);
+        rp[1] = make_uint4(__float_as_uint(v.z), __float_as_uint(v.w), s >> 16, 0u);
       }
     }
     if constexpr (!STATS) continue;
@@ -294,11 +300,14 @@ __global__ __launch_bounds__(256) void cbsr_stats_kernel(const float* __restrict
 // x[3j+1], x[3j+2], selectors 3j..3j+2 in bytes 0..2 of the 4th word}, so ONE dwordx4 gather
 // gives a lane its 3 values and their selectors (the 4-values-per-lane records need a
 // second, selector, gather per lane). Padding slots (3j+i >= k) are 0.
+template <int V>
 __global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
                                   const uint8_t* __restrict__ sp_index,
                                   uint8_t* __restrict__ rec, int ncols, int k, int rec_bytes,
                                   int ds, int is) {
-  const int chunks = (k + 2) / 3;
+  // V = 3: lane chunks {3 values, their 3 selector bytes}; V = 2: pair chunks {2 values, their
+  // 2 selector bytes, 0} (plan->fwd_chunk2)
+  const int chunks = (k + V - 1) / V;
   const int64_t total = (int64_t)ncols * chunks;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -306,11 +315,11 @@ __global__ void pack_cbsr3_kernel(const float* __restrict__ sp_data,
     const int j = (int)(t - c * chunks);
     uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int l = 3 * j + i;
+    for (int i = 0; i < V; ++i) {
+      const int l = V * j + i;
       if (l < k) {
         w[i] = __float_as_uint(sp_data[c * ds + l]);
-        w[3] |= (uint32_t)sp_index[c * is + l] << (8 * i);
+        w[V == 3 ? 3 : 2] |= (uint32_t)sp_index[c * is + l] << (8 * i);
       }
     }
     *reinterpret_cast<uint4*>(rec + c * rec_bytes + j * 16) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -339,6 +348,7 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
                                            int k, double sc) {
   using T = typename A::T;
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
+  constexpr bool C2 = (FL & kFwdFlagChunk2) != 0;
   constexpr bool EM = (FL & kFwdFlagQuad) != 0;
   const int last = e1 - 1;
   const int qq = threadIdx.x & 3;
@@ -385,6 +395,10 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
         const uint4 w = *reinterpret_cast<const uint4*>(rp + l0 * 16);
         x[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), 0.f);
         sel[u] = w.w;
+      } else if constexpr (C2) {  // pair chunk: 2 values + their selector bytes, one gather
+        const uint4 w = *reinterpret_cast<const uint4*>(rp + l0 * 16);
+        x[u] = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), 0.f, 0.f);
+        sel[u] = w.z;
       } else {
         x[u] = *reinterpret_cast<const float4*>(rp + l0 * 4);
         // two tables (plan->fwd_two_tables): values straight from sp_data, selectors from
@@ -410,6 +424,9 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
         A::add2(arow + (sv & 0xffu), vu, x[u].x);
         if (3 * l0 + 1 < k) A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
         if (3 * l0 + 2 < k) A::add2(arow + ((sv >> 16) & 0xffu), vu, x[u].z);
+      } else if constexpr (C2) {  // l0 = chunk index: slots 2 l0, 2 l0 + 1 (k even)
+        A::add2(arow + (sv & 0xffu), vu, x[u].x);
+        A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
       } else {
         A::add2(arow + (sv & 0xffu), vu, x[u].x);
         A::add2(arow + ((sv >> 8) & 0xffu), vu, x[u].y);
@@ -480,12 +497,13 @@ __global__ __launch_bounds__(NT) void spgemm_fwd_kernel(
   __syncthreads();
 
   constexpr bool C3 = (FL & kFwdFlagChunk3) != 0;
-  const int L = (VEC == 4) ? (C3 ? (k + 2) / 3 : k / 4) : (k < kWave ? k : kWave);
+  constexpr bool C2 = (FL & kFwdFlagChunk2) != 0;
+  const int L = (VEC == 4) ? (C3 ? (k + 2) / 3 : C2 ? k / 2 : k / 4) : (k < kWave ? k : kWave);
   const int EPS = kWave / L;  // edges per wave instruction
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int slot = lane / L;
-  const int l0 = (lane - slot * L) * (C3 ? 1 : VEC);
+  const int l0 = (lane - slot * L) * (C3 || C2 ? 1 : VEC);
   const bool lane_on = slot < EPS;
   constexpr int kWaves = NT / kWave;
 
@@ -1152,7 +1170,7 @@ static int launch_cbsr_stats(const float* sp_data, int ds, const uint8_t* sp_ind
                              int64_t nrows, int k, uint32_t* st0, uint32_t* st1, int cus,
                              hipStream_t s, uint8_t* rec = nullptr, int rec_bytes = 0,
                              const int32_t* zrows = nullptr, int nz = 0, float* out = nullptr,
-                             int D = 0) {
+                             int D = 0, bool pairs = false) {
   if (nrows <= 0) return MAXK_OK;
   if (k % 4 == 0) {
     const int64_t rows_per_block = (256 / kWave) * (kWave / (k / 4));
@@ -1161,15 +1179,15 @@ static int launch_cbsr_stats(const float* sp_data, int ds, const uint8_t* sp_ind
     const int cap = st0 ? cus * kStatsBlocksPerCu : 8 * cus;
     const int grid = (int)std::max<int64_t>(
         1, std::min<int64_t>((nrows + rows_per_block - 1) / rows_per_block, cap));
-    if (rec && st0)
-      hipLaunchKernelGGL((cbsr_stats4_kernel<true, true>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D, ds, is);
-    else if (rec)
-      hipLaunchKernelGGL((cbsr_stats4_kernel<true, false>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D, ds, is);
-    else
-      hipLaunchKernelGGL((cbsr_stats4_kernel<false, true>), dim3(grid), dim3(256), 0, s, sp_data,
-                         sp_index, nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D, ds, is);
+#define STATS4(PK, ST)                                                                      \
+  hipLaunchKernelGGL((cbsr_stats4_kernel<PK, ST>), dim3(grid), dim3(256), 0, s, sp_data, sp_index, \
+                     nrows, k, st0, st1, rec, rec_bytes, zrows, nz, out, D, ds, is)
+    if (rec && st0 && pairs) STATS4(2, true);
+    else if (rec && pairs) STATS4(2, false);
+    else if (rec && st0) STATS4(1, true);
+    else if (rec) STATS4(1, false);
+    else STATS4(0, true);
+#undef STATS4
   } else {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nrows + 255) / 256, 2 * cus));
     hipLaunchKernelGGL(cbsr_stats_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index, nrows,
@@ -1238,7 +1256,7 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   const size_t lds = fwd_lds_bytes(plan->fwd_tile_rows, D);
   // the caller's tables are already interleaved CBSR records {k values, k selectors} (the
   // multi-GPU path all-gathers them so): gather from them as they are, no per-call pack
-  const bool inplace = k % 4 == 0 && !plan->fwd_chunk3 &&
+  const bool inplace = k % 4 == 0 && !plan->fwd_chunk3 && !plan->fwd_chunk2 &&
                        sp_index == reinterpret_cast<const uint8_t*>(sp_data) + 4 * (size_t)k &&
                        is == 4 * ds;
   // two tables: values read straight from sp_data (ds floats per row), selectors from sp_index
@@ -1266,12 +1284,18 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
       xstat = st;
     }
   }
+  // pair chunks: packed by the statistics / pack pass when k % 4 == 0, else on their own;
+  // interleaved records are repacked too (W = 8 shard at k = 16: 0.356 ms compute with the
+  // repack against 0.358 gathering the records in place, profiles/r06/fwd_pair_chunks.jsonl)
+  const bool pairs = plan->fwd_chunk2;
   const bool pack4 = !two && !inplace && !plan->fwd_chunk3 && k % 4 == 0 && plan->num_cols > 0;
-  if (plan->fwd_chunk3 && plan->num_cols > 0) {
-    const int64_t items = (int64_t)plan->num_cols * ((k + 2) / 3);
+  if ((plan->fwd_chunk3 || (pairs && k % 4 != 0)) && plan->num_cols > 0) {
+    const int V = plan->fwd_chunk3 ? 3 : 2;
+    const int64_t items = (int64_t)plan->num_cols * ((k + V - 1) / V);
     const int grid = (int)std::min<int64_t>((items + 255) / 256, 65536);
-    hipLaunchKernelGGL(pack_cbsr3_kernel, dim3(grid), dim3(256), 0, s, sp_data, sp_index,
-                       rec_ws, plan->num_cols, k, plan->fwd_rec_bytes, ds, is);
+    hipLaunchKernelGGL(V == 3 ? pack_cbsr3_kernel<3> : pack_cbsr3_kernel<2>, dim3(grid), dim3(256),
+                       0, s, sp_data, sp_index, rec_ws, plan->num_cols, k, plan->fwd_rec_bytes,
+                       ds, is);
     MAXK_LAUNCH_CHECK("pack_cbsr3 launch");
   }
   const bool zero_in_stats = (pack4 || st) && k % 4 == 0;
@@ -1283,13 +1307,14 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
     const int rc2 = launch_cbsr_stats(sp_data, ds, sp_index, is, plan->num_cols, k, st,
                                       st ? st + 32 : nullptr, plan->cus, s,
                                       pack4 ? rec_ws : nullptr, plan->fwd_rec_bytes,
-                                      plan->zero_rows, zero_in_stats ? nz : 0, out, D);
+                                      plan->zero_rows, zero_in_stats ? nz : 0, out, D, pairs);
     if (rc2) return rc2;
   }
   if (plan->n_fwd_tasks == 0) return MAXK_OK;
-  const int Lf = plan->fwd_chunk3 ? (k + 2) / 3 : k / 4;  // lanes per edge
-  const int FL = (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0) |
+  const int Lf = plan->fwd_chunk3 ? (k + 2) / 3 : pairs ? k / 2 : k / 4;  // lanes per edge
+  const int FL = (plan->fwd_chunk3 ? kFwdFlagChunk3 : 0) | (pairs ? kFwdFlagChunk2 : 0) |
                  (plan->fwd_quad && Lf % 4 == 0 ? kFwdFlagQuad : 0);
+  const int fwaves = plan->fwd_waves;
 #define FWD_LAUNCH_NT(V, FF, NT, FU)                                                        \
   do {                                                                                      \
     if (lds > 64 * 1024) MAXK_HIP_TRY(allow_lds(spgemm_fwd_kernel<V, FF, NT, FU>, lds));     \
@@ -1301,15 +1326,17 @@ static int spgemm_forward_impl(const maxk_plan* plan, const int32_t* ptr, const 
   } while (0)
 #define FWD_LAUNCH(V, FF)                                                                   \
   do {                                                                                      \
-    if (plan->fwd_waves == 8 && plan->fwd_unroll == 4) FWD_LAUNCH_NT(V, FF, 8 * kWave, 4);   \
-    else if (plan->fwd_waves == 8) FWD_LAUNCH_NT(V, FF, 8 * kWave, kFwdUnroll);             \
+    if (fwaves == 8 && plan->fwd_unroll == 4) FWD_LAUNCH_NT(V, FF, 8 * kWave, 4);            \
+    else if (fwaves == 8) FWD_LAUNCH_NT(V, FF, 8 * kWave, kFwdUnroll);                      \
     else FWD_LAUNCH_NT(V, FF, kFwdThreads, kFwdUnroll);                                     \
   } while (0)
-  if (k % 4 == 0 || plan->fwd_chunk3) {
+  if (k % 4 == 0 || plan->fwd_chunk3 || plan->fwd_chunk2) {
     switch (FL) {
       case 0: FWD_LAUNCH(4, 0); break;
       case kFwdFlagChunk3: FWD_LAUNCH(4, kFwdFlagChunk3); break;
       case kFwdFlagQuad: FWD_LAUNCH(4, kFwdFlagQuad); break;
+      case kFwdFlagChunk2: FWD_LAUNCH(4, kFwdFlagChunk2); break;
+      case kFwdFlagChunk2 | kFwdFlagQuad: FWD_LAUNCH(4, kFwdFlagChunk2 | kFwdFlagQuad); break;
       default: FWD_LAUNCH(4, kFwdFlagChunk3 | kFwdFlagQuad); break;
     }
   } else {

@@ -658,6 +658,10 @@ PLAN_OPTIONS = [
     dict(bwd_waves=12, bwd_tasks_per_cu=32, bwd_min_task_edges=256),
     # lane-chunk forward records, two tables, fixed point / f64 with each forward layout
     dict(fwd_chunk3=1), dict(fwd_chunk3=2), dict(fwd_chunk3=1, fwd_fixed=2),
+    # pair-chunk forward records {2 values, 2 selectors} (round 6), fixed point and f64, 4 / 8
+    # waves (odd k falls back to the default layouts)
+    dict(fwd_chunk3=3), dict(fwd_chunk3=3, fwd_fixed=2), dict(fwd_chunk3=3, fwd_waves=8),
+    dict(fwd_chunk3=3, fwd_tile_rows=1),
     dict(fwd_two_tables=1), dict(fwd_two_tables=2), dict(fwd_two_tables=1, fwd_fixed=2),
     dict(fwd_fixed=2), dict(fwd_fixed=1, fwd_chunk3=1), dict(fwd_fixed=1, fwd_tile_rows=64),
     dict(fwd_fixed=1, fwd_two_tables=1), dict(fwd_fixed=1, fwd_rotate=2),
@@ -690,7 +694,7 @@ REMOVED_OPTIONS = [
 ]
 INVALID_OPTIONS = [
     dict(bwd_unroll=7), dict(bwd_unroll=4), dict(bwd_slot_groups=3), dict(fwd_tile_rows=65),
-    dict(bwd_lds_bytes=1 << 20), dict(bwd_algo=4), dict(bwd_waves=20), dict(fwd_chunk3=3),
+    dict(bwd_lds_bytes=1 << 20), dict(bwd_algo=4), dict(bwd_waves=20), dict(fwd_chunk3=4),
     dict(bwd_handout=3), dict(fwd_handout=-1), dict(fwd_waves=6), dict(fwd_waves=16),
     dict(fwd_waves=4, fwd_unroll=4),
     dict(fwd_two_tables=3), dict(bwd_flush=3), dict(bwd_piece_edges=-1), dict(bwd_chunk_bounds=4),
@@ -699,16 +703,21 @@ INVALID_OPTIONS = [
 ]
 
 
-@pytest.mark.parametrize("k,fw,fu,fh", [(8, 8, 8, 2), (16, 4, 8, 2), (32, 8, 8, 2), (48, 8, 4, 2),
+@pytest.mark.parametrize("k,fw,fu,fh", [(8, 8, 8, 2), (16, 8, 8, 2), (32, 8, 8, 2), (48, 8, 4, 2),
                                          (64, 8, 8, 2)])
 def test_plan_info_reports_launch_shapes(gpu, k, fw, fu, fh):
-    """Round-5 defaults: 8 forward waves with the counter hand-out except
-    4 at k = 16, 4 sub-steps at k = 48; 16 backward waves with the counter."""
+    """Defaults: 8 forward waves with the counter hand-out, 4
+    sub-steps at k = 48; pair chunks at k = 16 (8 waves; the packed records that replace them
+    with fwd_chunk3 = 2 take 4); 16 backward waves with the counter."""
     p, ix, v = GRAPHS["heavy_split"]()
     n = p.size - 1
     ptr, idx, val = graph_on(gpu, p, ix, v)
     info = mk.GraphPlan(ptr, idx, val, n, ix.size, 256, k).info()
     assert (info["fwd_waves"], info["fwd_unroll"], info["fwd_handout"]) == (fw, fu, fh)
+    if k == 16:
+        assert info["fwd_layout"] == 4
+        rec = mk.GraphPlan(ptr, idx, val, n, ix.size, 256, k, options={"fwd_chunk3": 2}).info()
+        assert rec["fwd_waves"] == 4 and rec["fwd_layout"] in (0, 1)  # tables: few edges/column
     assert (info["bwd_waves"], info["bwd_unroll"], info["bwd_handout"]) == (16, 8, 2)
     st = mk.GraphPlan(ptr, idx, val, n, ix.size, 256, k, options={"bwd_handout": 1}).info()
     assert st["bwd_waves"] in (8, 12) and st["bwd_handout"] == 1
@@ -985,7 +994,7 @@ def test_maxk_aggregate_fused_equals_unfused(gpu, k, mode):
     one bitwise where the forward is fixed point (k >= 16: integer sums, the same statistics);
     both outputs and both input gradients within the oracle bound (the backward's f32 LDS
     accumulation order varies from run to run); plan layouts covered: lane chunks (k = 8, 24),
-    packed records (16), two tables (32, 64)."""
+    pair chunks (16), two tables (32, 64)."""
     pt, it = graphs.synthetic_csr(2000, 300_000, seed=37)   # 150 edges per column: k = 16
     p, ix, v = pt.numpy(), it.numpy(), graphs.sage_mean_values(pt).numpy()  # packs records
     n, d = p.size - 1, 256
@@ -994,7 +1003,7 @@ def test_maxk_aggregate_fused_equals_unfused(gpu, k, mode):
     g = graphs.features(n, d, seed=32 + k).to(gpu)
     graph = mk.CSRGraph(*graph_on(gpu, p, ix, v))
     layout = graph.plan(d, k).info()["fwd_layout"]
-    assert layout == {8: 2, 24: 2, 16: 1, 32: 0, 64: 0}[k]
+    assert layout == {8: 2, 24: 2, 16: 4, 32: 0, 64: 0}[k]
     x1 = x.to(gpu).requires_grad_(True)
     y1 = mk.maxk_aggregate(x1, graph, k, mode)
     y1.backward(g)
