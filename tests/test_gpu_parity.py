@@ -311,6 +311,34 @@ def test_spgemm_forward_duplicate_selectors_summed(gpu):
     ptr, idx, val = graph_on(gpu, p, ix, v)
     out, _ = mk.spgemm_forward(ptr, idx, val, to_dev(data, gpu), to_dev(index, gpu), 2, 3, 4, 8)
     assert_close(out, ref, mag)
+    for fixed in (1, 2):   # pair chunks: both selectors of a chunk name the same slot
+        plan = mk.GraphPlan(ptr, idx, val, 2, 3, 8, 4,
+                            options={"fwd_chunk3": 3, "fwd_fixed": fixed})
+        assert_close(plan.forward(to_dev(data, gpu), to_dev(index, gpu)), ref, mag)
+
+
+@pytest.mark.parametrize("gname", ["synthetic", "heavy_split", "empty_rows", "single_node",
+                                   "no_edges"])
+@pytest.mark.parametrize("k", [2, 6, 8, 10, 14, 16, 18, 24, 32, 64, 128])
+@pytest.mark.parametrize("mode", ["exact", "ref_compat"])
+def test_spgemm_forward_pair_chunks_vs_oracle(gpu, gname, k, mode):
+    """Pair-chunk records (the k = 16 default, fwd_chunk3 = 3 at any even k up
+    to 128): quad-shared edge words when k / 2 % 4 == 0, the pack fused into the statistics
+    pass when k % 4 == 0 and on its own otherwise; fixed point and f64 accumulation; ref_compat
+    tables (rows with fewer than k entries over the threshold repeat selector 0 with value 0)."""
+    p, ix, v = GRAPHS[gname]()
+    n, d = p.size - 1, 256
+    x = graphs.features(n, d, seed=k + 11)
+    if mode == "ref_compat":
+        x[::3, : d // 2] = 0.0   # few entries above the bisection threshold on these rows
+    od, oi = oracle.maxk(x.numpy(), k, mode=mode)
+    ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    for fixed in (0, 1, 2):
+        plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, k,
+                            options={"fwd_chunk3": 3, "fwd_fixed": fixed})
+        assert plan.info()["fwd_layout"] == 4
+        assert_close(plan.forward(to_dev(od, gpu), to_dev(oi, gpu)), ref, mag)
 
 
 def _fwd_both_paths(gpu, p, ix, v, od, oi, d, k, **opts):
