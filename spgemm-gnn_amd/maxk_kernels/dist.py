@@ -10,8 +10,9 @@ exchange per direction:
 * forward : ONE RCCL all-gather of the k-sparse CBSR block as interleaved records
   {k f32 values, k u8 selectors} per row (5k bytes at k % 4 == 0), straight into the table
   the kernels read: the forward gathers these records in place (no per-call record pack over
-  the N columns; maxk_spgemm_forward_tables) and the backward reads the selectors at the
-  record stride. The rank's top-k is written straight into its send records
+  the N columns; maxk_spgemm_forward_tables), except at k = 16, where the plan's pair-chunk
+  layout repacks them in one pass without statistics (W = 8 shard 0.356 against
+  0.358 ms in place), and the backward reads the selectors at the record stride. The rank's top-k is written straight into its send records
   (``local_buffers`` + maxk_topk_cbsr_tables), so the exchange moves no extra copies. Then
   the local SpGEMM over the rank's rows with a rectangular plan whose column ids are
   remapped into the gathered table (once, at partition time);
