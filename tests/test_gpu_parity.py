@@ -282,7 +282,8 @@ def test_spgemm_forward_vs_oracle(gpu, gname, d, k):
     assert_close(out, ref, mag)
 
 
-@pytest.mark.parametrize("n,row", [(48, 47), (48, 32), (33, 32), (64, 63), (100, 70)])
+@pytest.mark.parametrize("n,row", [(48, 47), (48, 32), (33, 32), (64, 63), (100, 70), (48, 39),
+                                   (80, 78)])
 @pytest.mark.parametrize("d,k", [(1, 1), (256, 16), (256, 8), (256, 32)])
 def test_spgemm_forward_edgeless_tiles_before_edges(gpu, n, row, d, k):
     """Every row before `row` is edgeless, so whole forward tiles share their (empty) first
