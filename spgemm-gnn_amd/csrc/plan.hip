@@ -656,13 +656,16 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
   // ms 32 / 38 / 39 rows (tools/fwd_opts_sweep.py, profiles/r06/fwd_tile_rows.jsonl): k = 16
   // 1.022 / 0.996 / 0.989, k = 64 2.844 / 2.824 / 2.818, k = 8 0.891 / 0.876 (38), k = 32
   // 1.572 / 1.549 (38); ogbn-proteins k = 16 0.666 / 0.659 (38); yelp 0.468 / 0.461 / 0.464;
-  // flickr 0.0666 / 0.0683 / 0.0680. 40 rows leave one work-group per CU: +43 %.
+  // flickr 0.0666 / 0.0683 / 0.0680. 40 rows leave one work-group per CU: +43 %. Only with
+  // enough tiles for >= 5 rounds of two per CU: fewer, larger tiles lengthen the last round
+  // (flickr, 89 K rows, +2 %; an 8-GPU Reddit shard, 29 K rows: forward 0.146-0.151 ->
+  // 0.155-0.163 ms per rank, profiles/r06/shard_w8_all_ranks_39rows.jsonl).
   const int fwd_row_bytes = (D + kFwdRowPad) * 8;
-  const int fwd_two_wg_rows = (kBwdLdsBudget / 2 - 256) / fwd_row_bytes;
-  const bool fwd_lds_two_wg = 3 * kFwdTileRows * fwd_row_bytes > kBwdLdsBudget;
+  const int fwd_two_wg_rows = std::min(kFwdMaxTileRows, (kBwdLdsBudget / 2 - 256) / fwd_row_bytes);
+  const bool fwd_lds_two_wg = 3 * kFwdTileRows * fwd_row_bytes > kBwdLdsBudget &&
+                              (int64_t)N >= (int64_t)fwd_two_wg_rows * 10 * cus;
   p->fwd_tile_rows = o.fwd_tile_rows ? o.fwd_tile_rows
-                     : fwd_lds_two_wg ? std::min(kFwdMaxTileRows, fwd_two_wg_rows)
-                                      : kFwdTileRows;
+                     : fwd_lds_two_wg ? fwd_two_wg_rows : kFwdTileRows;
   // 8 waves per forward work-group, their windows from an LDS counter (below): more gathers
   // in flight per CU (Reddit k = 8 / 32 / 64 -4 / -7 / -9 %, k = 20..60 -4..-24 %), except
   // where the 4-wave sweep's column span is what keeps the records in L2: k = 16 (8 waves
