@@ -603,6 +603,27 @@ def test_plan_info(gpu):
     assert info["fwd_tasks"] > 0 and info["bwd_tasks"] >= info["bwd_blocks"]
 
 
+@pytest.mark.parametrize("n,d,rows", [(120_000, 256, 39), (50_000, 256, 32), (120_000, 128, 32),
+                                      (130_000, 212, 32), (130_000, 213, 47)])
+def test_forward_tile_rows_default(gpu, n, d, rows):
+    """Default forward tile: the most rows two work-groups per CU hold in LDS
+    (39 at D = 256) where the 32-row tile already allowed only two (D >= 213) and the graph
+    has rows for >= 5 rounds of them (>= 10 x 256 CUs x rows), else 32. Four edges per row, so
+    fwd_tasks = ceil(n / rows); the 39- and 47-row forwards checked against the oracle."""
+    rs = np.random.RandomState(n + d)
+    p = (np.arange(n + 1, dtype=np.int64) * 4).astype(np.int32)
+    ix = rs.randint(0, n, p[-1]).astype(np.int32)
+    v = rs.rand(ix.size).astype(np.float32)
+    ptr, idx, val = graph_on(gpu, p, ix, v)
+    plan = mk.GraphPlan(ptr, idx, val, n, ix.size, d, 16)
+    assert plan.info()["fwd_tasks"] == -(-n // rows)
+    if rows > 32:
+        x = graphs.features(n, d, seed=d)
+        od, oi = oracle.maxk(x.numpy(), 16)
+        ref, mag = oracle.spgemm_forward(p, ix, v, od, oi, d, with_mag=True)
+        assert_close(plan.forward(to_dev(od, gpu), to_dev(oi, gpu)), ref, mag)
+
+
 # ------------------------------------------------------------------------ autograd
 def test_autograd_matches_dense_torch(gpu):
     p, ix, v = GRAPHS["synthetic"]()
