@@ -885,7 +885,11 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
         if (e == hipSuccess)
           e = hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_kin, d_kout, d_ids, p->fwd_perm,
                                                  (int)E, 0, cbits + tbits, s);
-        if (e == hipSuccess) e = plan_malloc(&p->fwd_cv, sizeof(uint2) * E);
+        // one word past the end, zero (column 0, row 0, value 0): the forward's 16-B edge-word
+        // loads read edges in pairs from an even index, and a masked lane still gathers the
+        // record of the column it read
+        if (e == hipSuccess) e = plan_malloc(&p->fwd_cv, sizeof(uint2) * (E + 1));
+        if (e == hipSuccess) e = hipMemsetAsync(p->fwd_cv + E, 0, sizeof(uint2), s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(gather_fwd_kernel, dim3(grid_for(E, 256)), dim3(256), 0, s, p->fwd_perm,
                            idx, d_rl, val, E, p->fwd_cv, true);
@@ -895,7 +899,7 @@ static int plan_create_impl(const int32_t* ptr, const int32_t* idx, const float*
       dfree(d_starts); dfree(d_ranks); dfree(d_row0s); dfree(d_rl); dfree(d_ids);
       dfree(d_kin); dfree(d_kout); dfree(d_tmp);
       PLAN_TRY(fe);
-      p->device_bytes += (int64_t)E * 12;
+      p->device_bytes += (int64_t)E * 12 + 8;
     }
     PLAN_TRY(hipMalloc(&p->fwd_tasks, sizeof(FwdTask) * ftasks.size()));
     PLAN_TRY(hipMemcpyAsync(p->fwd_tasks, ftasks.data(), sizeof(FwdTask) * ftasks.size(),

@@ -361,12 +361,27 @@ __device__ __forceinline__ void fwd_edges4(typename A::T* acc, int e0, int e1, i
       if ((threadIdx.x & (kWave - 1)) == 0) c = atomicAdd(ctr, 1);
       wi = __builtin_amdgcn_readlane(c, 0);
     }
-    const int base = e0 + wi * (EPS * U);
+    const int base = (EM && U == 8 ? (e0 & ~1) : e0) + wi * (EPS * U);
     if (base >= e1) break;
     uint32_t cw[U];
     float v[U];
     bool ok[U];
-    if constexpr (EM) {
+    if constexpr (EM && U == 8) {
+      // eight sub-steps per quad from one 16-B load per lane (two edge words, lane q: sub-steps
+      // 2q, 2q + 1). Windows start at even edges (from e0 rounded down; cv holds E + 1 words,
+      // so the pair at the last edge stays in bounds); words outside [e0, e1) are masked, with
+      // their row bits dropped so their zero adds land in row 0 of this tile
+      const int sb = base + slot * U;
+      const uint4 wq = *reinterpret_cast<const uint4*>(cv + min(sb + 2 * qq, last & ~1));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t w0 = quad_pick((u & 1) ? wq.z : wq.x, u >> 1);
+        const uint32_t w1 = quad_pick((u & 1) ? wq.w : wq.y, u >> 1);
+        ok[u] = lane_on && sb + u >= e0 && sb + u < e1;
+        cw[u] = ok[u] ? w0 : (w0 & kFwdColMask);
+        v[u] = __uint_as_float(w1);
+      }
+    } else if constexpr (EM) {
       uint2 wq[U / 4];
 #pragma unroll
       for (int j = 0; j < U / 4; ++j) wq[j] = cv[min(base + slot * U + 4 * j + qq, last)];
