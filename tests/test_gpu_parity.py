@@ -711,7 +711,8 @@ PLAN_OPTIONS = [
     # pair-chunk forward records {2 values, 2 selectors} (round 6), fixed point and f64, 4 / 8
     # waves (odd k falls back to the default layouts)
     dict(fwd_chunk3=3), dict(fwd_chunk3=3, fwd_fixed=2), dict(fwd_chunk3=3, fwd_waves=8),
-    dict(fwd_chunk3=3, fwd_tile_rows=1),
+    dict(fwd_chunk3=3, fwd_tile_rows=1), dict(fwd_tile_rows=39), dict(fwd_tile_rows=39, fwd_chunk3=3),
+    dict(fwd_tile_rows=47, fwd_chunk3=2),
     dict(fwd_two_tables=1), dict(fwd_two_tables=2), dict(fwd_two_tables=1, fwd_fixed=2),
     dict(fwd_fixed=2), dict(fwd_fixed=1, fwd_chunk3=1), dict(fwd_fixed=1, fwd_tile_rows=64),
     dict(fwd_fixed=1, fwd_two_tables=1), dict(fwd_fixed=1, fwd_rotate=2),
